@@ -1,0 +1,185 @@
+"""Benchmark: FTRL timesteps/s at d=64, T=1e4 (BASELINE.json metric) on 1..N MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
+
+A step = one launch of the FTRL kernel (main T-step loop + comparator pass) over
+one resident batch of B sequences per GPU (default B = 32768: a 168 GB resident
+chunk of configs[2]'s 1e5-trial job).  Inputs are the reference's g(T) adversary
+(_rng(0, T, run) streams, fast_algorithms.py:231-239, d = 64) generated ON DEVICE
+before the timed region.  Each rank simulates its own runs (weak scaling, no
+data-path collective); each step ends with one all-gather of the regrets to
+collect the regret vector (the only exchange the path has).
+
+Printed (rank 0, one JSON line): value = all ranks' timesteps / max-over-ranks
+time; roofline of the kernel from HIP events on its stream (algorithmic bytes =
+2·(8d+8) per timestep); cpu_baseline = oracle/ocx_oracle.c (C port of
+_simulate_alg_core) single-threaded on a bounded sample of the same sequences; the
+parity error of the GPU regrets against that CPU sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--B", type=int, default=32768, help="sequences per GPU (resident batch)")
+    ap.add_argument("--T", type=int, default=10000)
+    ap.add_argument("--d", type=int, default=64)
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per sequence (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the CPU-baseline sample (0 disables)")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def cpu_baseline(T, d, runs, budget_s):
+    """Oracle (C restatement, 1 thread) on the first sequences of the same workload."""
+    from oracle import oracle as O
+    O.lib()
+    regs, steps, spent = [], 0, 0.0
+    r = 0
+    while spent < budget_s and r < runs:
+        z, y = O.gT_sample(0, T, r, d)
+        t0 = time.perf_counter()
+        reg = O.simulate_alg(z, y, 0, math.sqrt(2))
+        spent += time.perf_counter() - t0
+        regs.append(reg)
+        steps += T
+        r += 1
+    return np.array(regs), steps / spent if spent > 0 else float("nan"), spent
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    from online_convex_optimization_amd import engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.current_stream(dev)
+
+    B, T, d = a.B, a.T, a.d
+    run0 = rank * B  # this rank's runs: weak scaling, disjoint streams
+    db = engine.DeviceBatch(B, T, d, lanes_per_seq=a.lanes, device=local, stream=stream)
+    tg0 = time.perf_counter()
+    db.generate_gT(base_seed=0, run0=run0)
+    torch.cuda.synchronize()
+    gen_s = time.perf_counter() - tg0
+    gathered = torch.zeros(world * B, dtype=torch.float64, device=dev) if world > 1 else None
+
+    def step():
+        db.simulate_alg(0, math.sqrt(2))
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, db.regret[:B])
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        db.simulate_alg(0, math.sqrt(2))
+        ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, db.regret[:B])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    regrets = db.regret[:B].cpu().numpy()
+    out = None
+    if rank == 0:
+        steps_per_launch = B * T
+        value = world * B * T * a.steps / elapsed
+        alg_bytes = steps_per_launch * 2 * (8 * d + 8)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        try:
+            with open(a.traffic) as f:
+                tr = json.load(f)
+            if (tr.get("B"), tr.get("T"), tr.get("d"), tr.get("P")) == (B, T, d, db.L.P):
+                traffic = tr.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        cpu = None
+        parity = None
+        if a.cpu_seconds > 0:
+            cregs, cps, spent = cpu_baseline(T, d, B, a.cpu_seconds)
+            err = np.abs(regrets[:len(cregs)] - cregs)
+            parity = {"n_checked": int(len(cregs)), "max_abs_err": float(err.max()),
+                      "max_rel_err": float((err / np.maximum(np.abs(cregs), 1e-300)).max()),
+                      "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs))}
+            cpu = {"value": cps, "unit": "timesteps/s", "cores": 1, "kind": "port",
+                   "sample": f"{len(cregs)} sequences of the same workload (d={d}, T={T}, "
+                             f"runs 0..{len(cregs) - 1}), oracle/ocx_oracle.c single thread, "
+                             f"{spent:.1f} s"}
+        out = {
+            "metric": "FTRL timesteps/sec (whole node) at d=64, T=1e4; max |regret-ref| error",
+            "value": value,
+            "unit": "timesteps/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: g(T) adversary (_rng(0,T,run) PCG64/ziggurat streams) "
+                    "regenerated on device",
+            "config": {"workload": "configs[2]: batched FTRL d=64 T=1e4 (1e5-trial job as "
+                                   "resident batches of B per GPU)",
+                       "B_per_gpu": B, "T": T, "d": d, "lanes_per_seq": int(db.L.P),
+                       "coords_per_lane": int(db.L.C), "parallelism": f"dp{world}",
+                       "z_bytes_per_gpu": db.z_bytes},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                         "kernel": "ocx_alg_kernel", "kernel_ms": kern_ms,
+                         "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "gen_seconds": gen_s,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

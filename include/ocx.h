@@ -1,0 +1,139 @@
+/*
+ * ocx.h — C ABI of the MI355X online-convex-optimization engine (libocx.so).
+ *
+ * Drop-in boundary for the reference's per-timestep FTRL/FTL hot path
+ * (revvu/online_convex_optimization, /root/reference).  The reference is pure
+ * Python: its "operator API" is the module-level functions that the drivers
+ * select by import (fast_driver.py:23-28 vs driver.py:22-27).  Every entry point
+ * below names the reference function it replaces; the ctypes binding a maintainer
+ * adds on the reference side is shown in INTEGRATION.md and implemented in
+ * online_convex_optimization_amd/_lib.py.
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes, no torch types.
+ *   - Every function returns 0 on success or a negative ocx_status; the message
+ *     of the last failure on the calling thread is available via ocx_last_error().
+ *   - "host" entry points take host (numpy) pointers, copy to device `device`, run
+ *     the HIP kernels and copy results back (synchronous).
+ *   - "dev" entry points take device pointers in the engine's tiled HBM layout
+ *     (see ocx_layout) and a hipStream_t passed as void* (NULL = default stream);
+ *     they are asynchronous and capture-safe (no allocation, no sync).
+ *   - All arithmetic is IEEE binary64 (dtype "f64").
+ *   - lanes_per_seq: 1 = "exact" (every sum in the reference's sequential order →
+ *     bit-identical results; one lane per sequence for d <= 64, above that the
+ *     running sum is handed from lane to lane, layout.chain = 1); 2..64 (power of 2) =
+ *     a sequence's coordinates split over that many lanes of one wavefront
+ *     (butterfly reductions; ~1e-16 relative to the reference); 0 = auto
+ *     (throughput: picks P from B and d).
+ */
+#ifndef OCX_H_
+#define OCX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum ocx_status {
+    OCX_OK = 0,
+    OCX_E_INVALID = -1,   /* bad argument / shape */
+    OCX_E_HIP = -2,       /* HIP runtime error (no device, launch failure, OOM) */
+    OCX_E_UNSUPPORTED = -3
+} ocx_status;
+
+/* Tiled HBM layout shared by the generator and the simulation kernels.
+ * A wave-group is 64 lanes = S sequences x P lanes; lane L = s*P + c owns
+ * coordinates [c*C, (c+1)*C) of sequence g*S + s.  For group g and step t the
+ * z tile is 64*C contiguous doubles stored [k = 0..C/2-1][lane 0..63][2], so one
+ * wave loads a step with C/2 fully coalesced 1 KiB dwordx4 instructions.
+ *   z_tiled[((g*T + t)*64*C) + k*128 + L*2 + e] = z[b][t][c*C + 2k + e]
+ *   y_tiled[(g*T + t)*S + s]                   = y[b][t]
+ * Padding (coordinates j >= d, sequences b >= B) holds zeros. */
+typedef struct ocx_layout {
+    int64_t B, T, d;  /* logical sizes */
+    int32_t P;        /* lanes per sequence (1..64, power of two) */
+    int32_t C;        /* coordinates per lane (even) */
+    int32_t S;        /* sequences per wave-group = 64 / P */
+    int32_t chain;    /* 1: exact mode with P > 1 (running sum passed lane to lane) */
+    int64_t Dp;       /* padded dimension P*C >= d */
+    int64_t G;        /* wave-groups = ceil(B / S) */
+    int64_t z_elems;  /* doubles in z_tiled = G*T*64*C */
+    int64_t y_elems;  /* doubles in y_tiled = G*T*S */
+} ocx_layout;
+
+/* ---- library / device ---------------------------------------------------- */
+int ocx_version(void);
+int ocx_last_error(char* buf, size_t len);
+int ocx_device_count(int* count);
+/* Fill *out for (B, T, d) and a lanes_per_seq request (0 = auto). */
+int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layout* out);
+
+/* ---- host entry points (numpy buffers in, results out) ------------------- */
+
+/* fast_algorithms.py:171-177 simulate_alg (→ _simulate_alg_core :88-115), batched
+ * over B independent sequences; also exact_ftl.py:230-277 _simulate_ftrl when
+ * `comparator` ([B][d], nullable) replaces the final FTL action.
+ *   z [B][T][d], y [B][T] (C-contiguous f64); alg_flag 0 = FTRL, else FTL.
+ *   regret/cum_loss/comp_loss [B] (each nullable); x_last [B][d] nullable =
+ *   the last action played (exact_ftl.py:276). */
+int ocx_simulate_alg_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                           int alg_flag, double eta0, const double* comparator, double* regret,
+                           double* cum_loss, double* comp_loss, double* x_last,
+                           int lanes_per_seq, int device);
+
+/* fast_algorithms.py:184-195 simulate_SMART_like (→ :118-164), batched; thresh [B].
+ * switch_step [B] nullable: the t at which the switch fired, or -1. */
+int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                             const double* thresh, double eta0, double* regret,
+                             int64_t* switch_step, int lanes_per_seq, int device);
+
+/* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
+ * cum_loss = sum_{t<T} 0.5|z_t.a_t - y_t|; comp_loss = sum_t 0.5|z_t.a_T - y_t|. */
+int ocx_replay_batch(const double* z, const double* y, const double* actions, int64_t B,
+                     int64_t T, int64_t d, double* cum_loss, double* comp_loss, int device);
+
+/* fast_algorithms.py:230-241 (the body of empirical_worst_case_thresholds for one T):
+ * regenerates on device the R sequences _rng(base_seed, T, run0 + r), r < R, with
+ * `d` coordinates (the reference hard-codes d = 5), runs FTRL(eta0) on each and
+ * returns the R regrets (host array).  Only the regrets leave the GPU. */
+int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                   double eta0, double* regrets, int lanes_per_seq, int device);
+
+/* ---- device entry points (tiled layout, caller-owned device memory) ------ */
+
+/* Re-tile device arrays z [B][T][d], y [B][T] into the layout. */
+int ocx_dev_pack(const ocx_layout* L, const double* z, const double* y, double* z_tiled,
+                 double* y_tiled, void* stream);
+
+/* fast_algorithms.py:231-239 sampler on device: sequence b of the layout is
+ * _rng(base_seed, T, run0 + b) → clipped N(0, I_d) rows and ±1 labels. */
+int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* z_tiled,
+                   double* y_tiled, void* stream);
+
+/* fast_algorithms.py:88-115 on device.  comparator [B][d] device, nullable.
+ * Outputs are device arrays [B] (nullable) and x_last [B][d] (nullable). */
+int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                         int alg_flag, double eta0, const double* comparator, double* regret,
+                         double* cum_loss, double* comp_loss, double* x_last, void* stream);
+
+/* fast_algorithms.py:118-164 on device; thresh [B] device. */
+int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                           const double* thresh, double eta0, double* regret,
+                           int64_t* switch_step, void* stream);
+
+/* exact_ftl.py:306-333 on device; a_tiled is the actions [B][T+1][d] tiled with a
+ * layout of T+1 steps (z/y use L, actions use La with La->T == L->T + 1). */
+int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_tiled,
+                   const double* y_tiled, const double* a_tiled, double* cum_loss,
+                   double* comp_loss, void* stream);
+
+/* Max over runs of regrets[B] (device) into *gmax (device), starting from 0.0
+ * as fast_algorithms.py:228,242-243 does. */
+int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OCX_H_ */

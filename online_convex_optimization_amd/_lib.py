@@ -1,0 +1,123 @@
+"""ctypes binding of libocx.so (include/ocx.h) — the reference-side FFI stub.
+
+This is exactly the binding a maintainer of the reference would add next to
+``fast_algorithms.py`` (INTEGRATION.md shows it in that setting).  There is no
+CPU fallback: if ``libocx.so`` is missing or no HIP device is usable, every call
+raises.  Build the library with ``python -m online_convex_optimization_amd._build``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("OCX_LIB", os.path.join(_HERE, "libocx.so"))
+
+c_dp = ctypes.POINTER(ctypes.c_double)
+c_i64p = ctypes.POINTER(ctypes.c_int64)
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_int = ctypes.c_int
+c_double = ctypes.c_double
+c_vp = ctypes.c_void_p
+
+
+class OCXError(RuntimeError):
+    """A libocx call failed (bad argument, HIP error, unsupported shape)."""
+
+
+class Layout(ctypes.Structure):
+    """Mirror of ``ocx_layout`` (include/ocx.h)."""
+    _fields_ = [("B", c_i64), ("T", c_i64), ("d", c_i64), ("P", ctypes.c_int32),
+                ("C", ctypes.c_int32), ("S", ctypes.c_int32), ("chain", ctypes.c_int32),
+                ("Dp", c_i64), ("G", c_i64), ("z_elems", c_i64), ("y_elems", c_i64)]
+
+    def __repr__(self):
+        return (f"Layout(B={self.B}, T={self.T}, d={self.d}, P={self.P}, C={self.C}, "
+                f"S={self.S}, Dp={self.Dp}, G={self.G}, chain={self.chain})")
+
+
+# name → (restype, argtypes); every symbol declared in include/ocx.h
+SIGNATURES = {
+    "ocx_version": (c_int, []),
+    "ocx_last_error": (c_int, [ctypes.c_char_p, ctypes.c_size_t]),
+    "ocx_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "ocx_layout_init": (c_int, [c_i64, c_i64, c_i64, c_int, ctypes.POINTER(Layout)]),
+    "ocx_simulate_alg_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_int, c_double, c_dp,
+                                       c_dp, c_dp, c_dp, c_dp, c_int, c_int]),
+    "ocx_simulate_smart_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_double, c_dp,
+                                         c_i64p, c_int, c_int]),
+    "ocx_replay_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_dp, c_int]),
+    "ocx_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp, c_int, c_int]),
+    "ocx_dev_pack": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ocx_dev_gen_gT": (c_int, [ctypes.POINTER(Layout), c_u64, c_i64, c_vp, c_vp, c_vp]),
+    "ocx_dev_simulate_alg": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp,
+                                     c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "ocx_dev_simulate_smart": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_double, c_vp,
+                                       c_vp, c_vp]),
+    "ocx_dev_replay": (c_int, [ctypes.POINTER(Layout), ctypes.POINTER(Layout), c_vp, c_vp, c_vp,
+                               c_vp, c_vp, c_vp]),
+    "ocx_dev_max_regret": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libocx.so (raises OCXError if it is missing: no fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise OCXError(f"libocx.so not found at {LIB_PATH}: the HIP extension is not "
+                               "built (python -m online_convex_optimization_amd._build)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    buf = ctypes.create_string_buffer(4096)
+    load().ocx_last_error(buf, len(buf))
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        kind = {-1: "invalid argument", -2: "HIP error", -3: "unsupported"}.get(rc, str(rc))
+        msg = f"{what}: {kind}: {last_error()}"
+        if rc == -1:
+            raise ValueError(msg)
+        raise OCXError(msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def device_count() -> int:
+    n = c_int(0)
+    call("ocx_device_count", ctypes.byref(n))
+    return int(n.value)
+
+
+def layout(B: int, T: int, d: int, lanes_per_seq: int = 0) -> Layout:
+    L = Layout()
+    call("ocx_layout_init", int(B), int(T), int(d), int(lanes_per_seq), ctypes.byref(L))
+    return L
+
+
+def ptr(a):
+    """ctypes double* of a C-contiguous float64 numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(c_dp)

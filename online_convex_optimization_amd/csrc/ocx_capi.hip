@@ -1,0 +1,382 @@
+// ocx_capi.hip — the extern "C" boundary (include/ocx.h): layout planning, per-device
+// workspaces for the host entry points, argument checking and error reporting.
+// Host code only; kernels live in ocx_sim.hip / ocx_gen.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/ocx.h"
+#include "ocx_sim_kernels.h"
+
+#define OCX_VERSION 100  // 0.1.0
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define OCX_HIP(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(OCX_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+constexpr int kMaxDevices = 64;
+
+// Grow-only device buffers for the host entry points (one set per device).
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct DevCtx {
+    std::mutex mu;
+    bool init = false;
+    hipStream_t stream = nullptr;
+    DevBuf zraw, yraw, zt, yt, at, araw, cmp, thr, out, sw;
+};
+
+DevCtx g_ctx[kMaxDevices];
+
+int ctx_enter(int device, DevCtx** out) {
+    int n = 0;
+    OCX_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n || device >= kMaxDevices)
+        return fail(OCX_E_INVALID, "device " + std::to_string(device) + " out of range (count " +
+                                       std::to_string(n) + ")");
+    OCX_HIP(hipSetDevice(device));
+    DevCtx* c = &g_ctx[device];
+    if (!c->init) {
+        OCX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->init = true;
+    }
+    *out = c;
+    return OCX_OK;
+}
+
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int even_supported_C(int64_t need) {
+    static const int Cs[] = {2, 4, 6, 8, 12, 16, 24, 32, 48, 64};
+    for (int c : Cs)
+        if (c >= need) return c;
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocx_version(void) { return OCX_VERSION; }
+
+int ocx_last_error(char* buf, size_t len) {
+    if (buf && len) {
+        std::snprintf(buf, len, "%s", g_err.c_str());
+    }
+    return (int)g_err.size();
+}
+
+int ocx_device_count(int* count) {
+    if (!count) return fail(OCX_E_INVALID, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(OCX_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *count = n;
+    return OCX_OK;
+}
+
+int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layout* L) {
+    if (!L) return fail(OCX_E_INVALID, "layout is NULL");
+    if (B < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative size");
+    if (d > 4096) return fail(OCX_E_UNSUPPORTED, "d > 4096 not supported");
+    int P = lanes_per_seq;
+    if (P == 0) {
+        // auto: the fewest lanes per sequence that still gives
+        // ~8 wavefronts per CU (131072 lanes on 256 CUs), clamped so a lane keeps
+        // >= 2 coordinates (no lane of pure padding) and <= 64 coordinates.
+        int64_t p_lanes = 1;
+        while (p_lanes < 64 && p_lanes * B < 131072) p_lanes *= 2;
+        int64_t p_min = 1;
+        while (p_min < 64 && ceil_div(d, p_min) > 64) p_min *= 2;
+        int64_t p_max = 1;
+        while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
+        P = (int)std::max(p_min, std::min(p_lanes, p_max));
+    }
+    if (P < 1 || P > 64 || (P & (P - 1)) != 0)
+        return fail(OCX_E_INVALID, "lanes_per_seq must be 0 or a power of two in [1, 64]");
+    int chain = 0;
+    int C;
+    if (P == 1 && d > 64) {
+        // exact mode above 64 coordinates: 64 per lane, running sum handed lane to lane
+        int64_t p = 2;
+        while (p < 64 && ceil_div(d, p) > 64) p *= 2;
+        if (ceil_div(d, p) > 64) return fail(OCX_E_UNSUPPORTED, "d too large for exact mode");
+        P = (int)p;
+        C = 64;
+        chain = 1;
+    } else {
+        C = even_supported_C(std::max<int64_t>(ceil_div(d, P), 1));
+        if (C < 0)
+            return fail(OCX_E_UNSUPPORTED,
+                        "d / lanes_per_seq > 64 coordinates per lane; use more lanes");
+    }
+    std::memset(L, 0, sizeof(*L));
+    L->B = B;
+    L->T = T;
+    L->d = d;
+    L->P = P;
+    L->C = C;
+    L->chain = chain;
+    L->S = 64 / P;
+    L->Dp = (int64_t)P * C;
+    L->G = ceil_div(B, L->S);
+    L->z_elems = L->G * T * 64 * (int64_t)C;
+    L->y_elems = L->G * T * L->S;
+    return OCX_OK;
+}
+
+// ---------------------------------------------------------------- device API
+static int check_layout(const ocx_layout* L) {
+    if (!L) return fail(OCX_E_INVALID, "layout is NULL");
+    if (!ocx_supported_C(L->C) || L->P < 1 || L->P > 64 || L->S * L->P != 64)
+        return fail(OCX_E_INVALID, "corrupt layout");
+    if (L->chain && L->C != 64) return fail(OCX_E_INVALID, "corrupt layout (chain needs C=64)");
+    return OCX_OK;
+}
+
+int ocx_dev_pack(const ocx_layout* L, const double* z, const double* y, double* z_tiled,
+                 double* y_tiled, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->z_elems && (!z_tiled || (L->B * L->T * L->d > 0 && !z)))
+        return fail(OCX_E_INVALID, "NULL z buffer");
+    if (L->y_elems && (!y_tiled || !y)) return fail(OCX_E_INVALID, "NULL y buffer");
+    OCX_HIP(ocx_launch_pack(L, z, y, z_tiled, y_tiled, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* z_tiled,
+                   double* y_tiled, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (run0 < 0) return fail(OCX_E_INVALID, "run0 < 0");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
+    OCX_HIP(ocx_launch_gen_gT(L, base_seed, run0, z_tiled, y_tiled, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                         int alg_flag, double eta0, const double* comparator, double* regret,
+                         double* cum_loss, double* comp_loss, double* x_last, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag, eta0, comparator, regret, cum_loss,
+                           comp_loss, x_last, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                           const double* thresh, double eta0, double* regret,
+                           int64_t* switch_step, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->B && (!thresh || !regret)) return fail(OCX_E_INVALID, "NULL thresh/regret");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    OCX_HIP(ocx_launch_smart(L, z_tiled, y_tiled, thresh, eta0, regret, switch_step,
+                             (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_tiled,
+                   const double* y_tiled, const double* a_tiled, double* cum_loss,
+                   double* comp_loss, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (int rc = check_layout(La)) return rc;
+    if (La->T != L->T + 1 || La->B != L->B || La->P != L->P || La->C != L->C ||
+        La->chain != L->chain)
+        return fail(OCX_E_INVALID, "actions layout must match z layout with T+1 steps");
+    if (L->B && (!a_tiled || !cum_loss || !comp_loss)) return fail(OCX_E_INVALID, "NULL buffer");
+    OCX_HIP(ocx_launch_replay(L, z_tiled, y_tiled, a_tiled, cum_loss, comp_loss,
+                              (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* stream) {
+    if (!gmax || (B > 0 && !regrets)) return fail(OCX_E_INVALID, "NULL buffer");
+    OCX_HIP(ocx_launch_max(regrets, B, gmax, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+// ---------------------------------------------------------------- host API
+int ocx_simulate_alg_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                           int alg_flag, double eta0, const double* comparator, double* regret,
+                           double* cum_loss, double* comp_loss, double* x_last,
+                           int lanes_per_seq, int device) {
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y)) return fail(OCX_E_INVALID, "NULL z/y");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * (3 + d) * 8));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    const double* dcmp = nullptr;
+    if (comparator) {
+        OCX_HIP(cx->cmp.ensure((size_t)B * d * 8 + 8));
+        if (B * d)
+            OCX_HIP(hipMemcpyAsync(cx->cmp.p, comparator, (size_t)B * d * 8,
+                                   hipMemcpyHostToDevice, st));
+        dcmp = cx->cmp.as<double>();
+    }
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    double* o = cx->out.as<double>();
+    double* dxl = x_last ? o + 3 * B : nullptr;
+    if (dxl && B * d) OCX_HIP(hipMemsetAsync(dxl, 0, (size_t)B * d * 8, st));
+    OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), alg_flag, eta0, dcmp, o,
+                           o + B, o + 2 * B, dxl, st));
+    std::vector<double> h((size_t)B * (3 + (x_last ? d : 0)));
+    OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    if (regret) std::memcpy(regret, h.data(), B * 8);
+    if (cum_loss) std::memcpy(cum_loss, h.data() + B, B * 8);
+    if (comp_loss) std::memcpy(comp_loss, h.data() + 2 * B, B * 8);
+    if (x_last && d) std::memcpy(x_last, h.data() + 3 * B, (size_t)B * d * 8);
+    return OCX_OK;
+}
+
+int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                             const double* thresh, double eta0, double* regret,
+                             int64_t* switch_step, int lanes_per_seq, int device) {
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || !thresh || !regret)
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->thr.ensure((size_t)B * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * 8));
+    OCX_HIP(cx->sw.ensure((size_t)B * 8));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(hipMemcpyAsync(cx->thr.p, thresh, (size_t)B * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    OCX_HIP(ocx_launch_smart(&L, cx->zt.as<double>(), cx->yt.as<double>(), cx->thr.as<double>(),
+                             eta0, cx->out.as<double>(), cx->sw.as<int64_t>(), st));
+    OCX_HIP(hipMemcpyAsync(regret, cx->out.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    if (switch_step)
+        OCX_HIP(hipMemcpyAsync(switch_step, cx->sw.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
+int ocx_replay_batch(const double* z, const double* y, const double* actions, int64_t B,
+                     int64_t T, int64_t d, double* cum_loss, double* comp_loss, int device) {
+    ocx_layout L, La;
+    if (int rc = ocx_layout_init(B, T, d, 1, &L)) return rc;
+    if (int rc = ocx_layout_init(B, T + 1, d, 1, &La)) return rc;
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || (d > 0 && !actions) || !cum_loss || !comp_loss)
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T), na = (size_t)(B * (T + 1) * d);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->araw.ensure(na * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->at.ensure((size_t)La.z_elems * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * 2 * 8));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    if (na) OCX_HIP(hipMemcpyAsync(cx->araw.p, actions, na * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    // actions are tiled like z with T+1 steps (no label part)
+    ocx_layout Lz = La;
+    Lz.y_elems = 0;
+    OCX_HIP(ocx_launch_pack(&Lz, cx->araw.as<double>(), nullptr, cx->at.as<double>(), nullptr, st));
+    double* o = cx->out.as<double>();
+    OCX_HIP(ocx_launch_replay(&L, cx->zt.as<double>(), cx->yt.as<double>(), cx->at.as<double>(), o,
+                              o + B, st));
+    OCX_HIP(hipMemcpyAsync(cum_loss, o, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipMemcpyAsync(comp_loss, o + B, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
+int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                   double eta0, double* regrets, int lanes_per_seq, int device) {
+    if (R < 0 || run0 < 0) return fail(OCX_E_INVALID, "negative run range");
+    if (R == 0) return OCX_OK;
+    if (!regrets) return fail(OCX_E_INVALID, "NULL regrets");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    // chunk the runs so the tiled z of one chunk stays <= ~16 GiB
+    const int64_t per_seq = std::max<int64_t>(T * (d + 1) * 8, 8);
+    int64_t chunk = std::max<int64_t>((int64_t)16 << 30, 0) / per_seq;
+    chunk = std::max<int64_t>(64, std::min<int64_t>(chunk, R));
+    OCX_HIP(cx->out.ensure((size_t)std::min(chunk, R) * 8));
+    for (int64_t r0 = 0; r0 < R; r0 += chunk) {
+        const int64_t nb = std::min(chunk, R - r0);
+        ocx_layout L;
+        if (int rc = ocx_layout_init(nb, T, d, lanes_per_seq, &L)) return rc;
+        OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+        OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+        OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(), cx->yt.as<double>(),
+                                  st));
+        OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
+                               cx->out.as<double>(), nullptr, nullptr, nullptr, st));
+        OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
+        OCX_HIP(hipStreamSynchronize(st));
+    }
+    return OCX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// ocx_internal.h — shared device helpers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ocx.h"
+
+#define OCX_WAVE 64
+#define OCX_BLOCK 256  // 4 wave-groups per workgroup
+#define OCX_WAVES_PER_BLOCK (OCX_BLOCK / OCX_WAVE)
+
+// ---------------------------------------------------------------------------
+// Cross-lane fp64 reductions over the P lanes that own one sequence.
+// All steps are symmetric butterflies (lane i: a+b, its partner: b+a), so every
+// lane of a sequence ends with the bit-identical total and takes the same
+// branch (norm > 1, sign of q - y) — the per-sequence control flow stays uniform.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ double ocx_dpp(double v) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double ocx_swz_xor16(double v) {
+    // ds_swizzle bit-mode: and 0x1F, or 0, xor 0x10 (within 32-lane halves)
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_ds_swizzle(lo, 0x401F);
+    hi = __builtin_amdgcn_ds_swizzle(hi, 0x401F);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double ocx_xor32(double v) {
+    int addr = ((int)(threadIdx.x & 63) ^ 32) << 2;
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_ds_bpermute(addr, lo);
+    hi = __builtin_amdgcn_ds_bpermute(addr, hi);
+    return __hiloint2double(hi, lo);
+}
+
+template <int P>
+__device__ __forceinline__ double ocx_seq_sum(double v) {
+    if constexpr (P >= 2) v = v + ocx_dpp<0xB1>(v);   // quad_perm [1,0,3,2]  (xor 1)
+    if constexpr (P >= 4) v = v + ocx_dpp<0x4E>(v);   // quad_perm [2,3,0,1]  (xor 2)
+    if constexpr (P >= 8) v = v + ocx_dpp<0x141>(v);  // row_half_mirror (quads are uniform)
+    if constexpr (P >= 16) v = v + ocx_dpp<0x140>(v); // row_mirror (half-rows are uniform)
+    if constexpr (P >= 32) v = v + ocx_swz_xor16(v);
+    if constexpr (P >= 64) v = v + ocx_xor32(v);
+    return v;
+}
+
+// Index of element (g, t, j-chunk pair k, lane L, e) in the tiled z layout.
+__host__ __device__ __forceinline__ int64_t ocx_ztile_base(int64_t g, int64_t T, int64_t t,
+                                                          int C) {
+    return (g * T + t) * (int64_t)(64 * C);
+}
+
+// Native 2 x f64 vector (one dwordx4 per lane); HIP's double2 is a struct, which
+// __builtin_nontemporal_load does not accept.
+typedef double ocx_d2 __attribute__((ext_vector_type(2)));

@@ -1,0 +1,242 @@
+// ocx_rng.h — NumPy-stream-compatible RNG for the g(T) adversary, host+device.
+//
+// Restates, for one lane = one independent stream, what the reference's `_rng`
+// (fast_algorithms.py:254-257, algorithms.py:177-180) builds through NumPy 2.x:
+//   Generator(PCG64(SeedSequence([base_seed, T, run])))
+// and the draws the g(T) sampler makes from it (fast_algorithms.py:234-239):
+//   standard_normal  → NumPy's 256-layer ziggurat (random_standard_normal),
+//   choice([-1,1])   → integers(0, 2) → buffered Lemire uint32 = top bit of each
+//                      32-bit half of a raw draw, low half first.
+// The same source compiles with g++ (tests/test_rng_host.py checks it against NumPy
+// on the CPU) and with hipcc for gfx950 (the generator kernel).
+#pragma once
+#include <stdint.h>
+
+#include "zig_tables.h"
+
+#if defined(__HIPCC__)
+#define OCX_HD __host__ __device__ __forceinline__
+#else
+#define OCX_HD static inline
+#include <math.h>
+#endif
+
+typedef unsigned __int128 ocx_u128;
+
+// ---------------------------------------------------------------------------
+// SeedSequence (numpy/random/bit_generator.pyx): pool_size 4, uint32 arithmetic.
+// ---------------------------------------------------------------------------
+#define OCX_SS_INIT_A 0x43b0d7e5u
+#define OCX_SS_MULT_A 0x931e8875u
+#define OCX_SS_INIT_B 0x8b51f9ddu
+#define OCX_SS_MULT_B 0x58f38dedu
+#define OCX_SS_MIX_L 0xca01f9ddu
+#define OCX_SS_MIX_R 0x4973f715u
+#define OCX_SS_MAX_WORDS 12
+
+OCX_HD uint32_t ocx_ss_hashmix(uint32_t value, uint32_t* hash_const) {
+    value ^= *hash_const;
+    *hash_const *= OCX_SS_MULT_A;
+    value *= *hash_const;
+    value ^= value >> 16;
+    return value;
+}
+
+OCX_HD uint32_t ocx_ss_mix(uint32_t x, uint32_t y) {
+    uint32_t r = OCX_SS_MIX_L * x - OCX_SS_MIX_R * y;
+    r ^= r >> 16;
+    return r;
+}
+
+// entropy: the concatenated uint32 words of every entropy integer (each integer
+// contributes ⌈bits/32⌉ words, little-endian, and 0 contributes one word 0).
+// Writes the 4 uint64 words of generate_state(4, np.uint64).
+OCX_HD void ocx_seedseq_state4(const uint32_t* entropy, int n, uint64_t out[4]) {
+    uint32_t pool[4];
+    uint32_t hc = OCX_SS_INIT_A;
+    for (int i = 0; i < 4; ++i) pool[i] = ocx_ss_hashmix(i < n ? entropy[i] : 0u, &hc);
+    for (int s = 0; s < 4; ++s)
+        for (int d = 0; d < 4; ++d)
+            if (s != d) pool[d] = ocx_ss_mix(pool[d], ocx_ss_hashmix(pool[s], &hc));
+    for (int s = 4; s < n; ++s)
+        for (int d = 0; d < 4; ++d) pool[d] = ocx_ss_mix(pool[d], ocx_ss_hashmix(entropy[s], &hc));
+    uint32_t w[8];
+    uint32_t hb = OCX_SS_INIT_B;
+    for (int i = 0; i < 8; ++i) {
+        uint32_t v = pool[i & 3];
+        v ^= hb;
+        hb *= OCX_SS_MULT_B;
+        v *= hb;
+        v ^= v >> 16;
+        w[i] = v;
+    }
+    for (int i = 0; i < 4; ++i) out[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+}
+
+// Append the uint32 words of a non-negative integer (numpy _int_to_uint32_array).
+OCX_HD int ocx_ss_push_int(uint32_t* words, int n, uint64_t v) {
+    if (v == 0) {
+        words[n++] = 0u;
+        return n;
+    }
+    while (v != 0) {
+        words[n++] = (uint32_t)v;
+        v >>= 32;
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------------------
+// PCG64 (XSL-RR 128/64), as numpy/random/src/pcg64: step, then output.
+// ---------------------------------------------------------------------------
+struct ocx_pcg64 {
+    ocx_u128 state;
+    ocx_u128 inc;
+    uint32_t buf32;   // buffered high half for next_uint32
+    int has32;
+};
+
+#define OCX_PCG_MULT ((((ocx_u128)0x2360ED051FC65DA4ULL) << 64) | (ocx_u128)0x4385DF649FCCF645ULL)
+
+OCX_HD void ocx_pcg_seed(ocx_pcg64* g, const uint64_t st4[4]) {
+    ocx_u128 s = (((ocx_u128)st4[0]) << 64) | st4[1];
+    ocx_u128 i = (((ocx_u128)st4[2]) << 64) | st4[3];
+    g->state = 0;
+    g->inc = (i << 1) | 1u;
+    g->state = g->state * OCX_PCG_MULT + g->inc;
+    g->state += s;
+    g->state = g->state * OCX_PCG_MULT + g->inc;
+    g->buf32 = 0;
+    g->has32 = 0;
+}
+
+OCX_HD uint64_t ocx_pcg_next64(ocx_pcg64* g) {
+    g->state = g->state * OCX_PCG_MULT + g->inc;
+    uint64_t hi = (uint64_t)(g->state >> 64);
+    uint64_t lo = (uint64_t)g->state;
+    unsigned rot = (unsigned)(g->state >> 122);
+    uint64_t x = hi ^ lo;
+    return (x >> rot) | (x << ((0u - rot) & 63u));
+}
+
+OCX_HD uint32_t ocx_pcg_next32(ocx_pcg64* g) {
+    if (g->has32) {
+        g->has32 = 0;
+        return g->buf32;
+    }
+    uint64_t v = ocx_pcg_next64(g);
+    g->has32 = 1;
+    g->buf32 = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+}
+
+OCX_HD double ocx_pcg_next_double(ocx_pcg64* g) {
+    return (double)(ocx_pcg_next64(g) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Seed one stream exactly as _rng(w0, w1, w2) = SeedSequence([w0, w1, w2]).
+OCX_HD void ocx_rng_init3(ocx_pcg64* g, uint64_t w0, uint64_t w1, uint64_t w2) {
+    uint32_t words[OCX_SS_MAX_WORDS];
+    int n = 0;
+    n = ocx_ss_push_int(words, n, w0);
+    n = ocx_ss_push_int(words, n, w1);
+    n = ocx_ss_push_int(words, n, w2);
+    uint64_t st[4];
+    ocx_seedseq_state4(words, n, st);
+    ocx_pcg_seed(g, st);
+}
+
+// ---------------------------------------------------------------------------
+// Ziggurat standard normal (NumPy random_standard_normal).  The three tables are
+// passed in so the device kernel can serve them from LDS.
+// ---------------------------------------------------------------------------
+#define OCX_ZIG_NOR_R 3.6541528853610087963519472518
+#define OCX_ZIG_NOR_INV_R 0.27366123732975827203338247596
+
+template <class KiT, class WiT, class FiT>
+OCX_HD double ocx_standard_normal(ocx_pcg64* g, const KiT& ki, const WiT& wi, const FiT& fi) {
+    for (;;) {
+        uint64_t r = ocx_pcg_next64(g);
+        int idx = (int)(r & 0xff);
+        r >>= 8;
+        int sign = (int)(r & 0x1);
+        uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
+        double x = (double)rabs * wi(idx);
+        if (sign & 0x1) x = -x;
+        if (rabs < ki(idx)) return x;
+        if (idx == 0) {
+            for (;;) {
+                double xx = -OCX_ZIG_NOR_INV_R * log1p(-ocx_pcg_next_double(g));
+                double yy = -log1p(-ocx_pcg_next_double(g));
+                if (yy + yy > xx * xx)
+                    return ((rabs >> 8) & 0x1) ? -(OCX_ZIG_NOR_R + xx) : OCX_ZIG_NOR_R + xx;
+            }
+        } else {
+            if (((fi(idx - 1) - fi(idx)) * ocx_pcg_next_double(g) + fi(idx)) < exp(-0.5 * x * x))
+                return x;
+        }
+    }
+}
+
+// NumPy pairwise_sum order for a row of n squares (numpy/_core/src/umath/loops_utils.h):
+// n < 8 sequential; 8 <= n <= 128 eight strided accumulators combined
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) then the n%8 tail sequentially; n > 128 split
+// at n2 = n/2 - (n/2)%8 and recurse.  ocx_pw_* evaluate that order while values
+// stream in one at a time: `ocx_pw_plan` lists the leaves (≤128-element blocks) in
+// order and the post-order combine program.
+#define OCX_PW_MAX_LEAVES 64
+struct ocx_pw_plan {
+    int nleaf;
+    int leaf_len[OCX_PW_MAX_LEAVES];
+    // program: sequence of ops; op >= 0 → push leaf #op; op == -1 → pop b, pop a, push a+b
+    int nops;
+    int ops[2 * OCX_PW_MAX_LEAVES];
+};
+
+OCX_HD void ocx_pw_build_rec(ocx_pw_plan* p, int n) {
+    if (n <= 128) {
+        p->ops[p->nops++] = p->nleaf;
+        p->leaf_len[p->nleaf++] = n;
+        return;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    ocx_pw_build_rec(p, n2);
+    ocx_pw_build_rec(p, n - n2);
+    p->ops[p->nops++] = -1;
+}
+
+OCX_HD void ocx_pw_build(ocx_pw_plan* p, int n) {
+    p->nleaf = 0;
+    p->nops = 0;
+    ocx_pw_build_rec(p, n);
+}
+
+// Sum of one leaf block of `n` (≤128) values in NumPy's order.
+struct ocx_pw_leaf {
+    double r[8];
+    double res;
+    int i, n, n8;
+};
+
+OCX_HD void ocx_pw_leaf_begin(ocx_pw_leaf* L, int n) {
+    for (int k = 0; k < 8; ++k) L->r[k] = 0.0;
+    L->res = 0.0;
+    L->i = 0;
+    L->n = n;
+    L->n8 = n - (n % 8);
+}
+
+OCX_HD void ocx_pw_leaf_add(ocx_pw_leaf* L, double v) {
+    if (L->n < 8) {
+        L->res += v;
+    } else if (L->i < L->n8) {
+        L->r[L->i & 7] += v;  // r[k] = a[k] + a[k+8] + ... (0.0 + a[k] is exact)
+        if (L->i + 1 == L->n8)
+            L->res = ((L->r[0] + L->r[1]) + (L->r[2] + L->r[3])) +
+                     ((L->r[4] + L->r[5]) + (L->r[6] + L->r[7]));
+    } else {
+        L->res += v;
+    }
+    L->i++;
+}

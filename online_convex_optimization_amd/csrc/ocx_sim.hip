@@ -1,0 +1,515 @@
+// ocx_sim.hip — gfx950 kernels for the per-timestep FTRL/FTL/SMART loops.
+//
+// One wavefront owns S = 64/P independent sequences; the P lanes of a sequence
+// hold C coordinates each of theta (registers), so the sequential T-step
+// recurrence runs entirely on chip and HBM sees only the streamed z_t / y_t tiles
+// (layout: include/ocx.h, ocx_layout).  Each step a wave loads one 512*C-byte tile
+// with C/2 coalesced 1 KiB dwordx4 loads, issued NB-1 steps ahead through a
+// register ring so the HBM latency hides behind the on-chip arithmetic.
+//
+// Arithmetic follows the reference's operation order per lane (sequential sums
+// from 0.0, IEEE sqrt/div, no contraction: built with -ffp-contract=off); with
+// P = 1 every sum is the reference's sequential sum and results are bit-identical
+// to fast_algorithms.py; with P > 1 the per-lane partial sums are combined by a
+// butterfly (ocx_seq_sum).
+#include <algorithm>
+
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+template <int C>
+__device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p) {
+#pragma unroll
+    for (int k = 0; k < C / 2; ++k) dst[k] = __builtin_nontemporal_load(p + k * 64);
+}
+
+__device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
+    return (j & 1) ? zb[j >> 1].y : zb[j >> 1].x;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Per-sequence totals of C per-lane products p[j] (coordinate c*C + j).
+//   tree  (CHAIN=false): lane-local sequential sum, then the P-lane butterfly;
+//   chain (CHAIN=true):  the running sum visits lanes 0..P-1 in order and each
+//         lane adds its products one by one → exactly the reference's sequential
+//         order over all d coordinates (exact mode for d > 64).
+// ---------------------------------------------------------------------------
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
+    if constexpr (!CHAIN || P == 1) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc += p[j];
+        return ocx_seq_sum<P>(acc);
+    } else {
+        const int c = lane % P;
+        const int base = lane - c;
+        double acc = 0.0;
+        for (int cc = 0; cc < P; ++cc) {
+            if (c == cc) {
+#pragma unroll
+                for (int j = 0; j < C; ++j) acc += p[j];
+            }
+            acc = __shfl(acc, base + cc, 64);
+        }
+        return acc;
+    }
+}
+
+__device__ __forceinline__ double ocx_grad(double diff) {  // fast_algorithms.py:27-34
+    return diff > 0.0 ? 0.5 : (diff < 0.0 ? -0.5 : 0.0);
+}
+
+// FTRL action (fast_algorithms.py:52-66): x = (s*theta) * f, f = 1/||s*theta|| if > 1
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ void ocx_action_ftrl(const double (&th)[C], int64_t t1, double eta0,
+                                                double (&x)[C], int lane) {
+    const double sc = -(eta0 / sqrt((double)t1));
+    double p[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        x[j] = sc * th[j];
+        p[j] = x[j] * x[j];
+    }
+    const double nsq = ocx_total<C, P, CHAIN>(p, lane);
+    const double f = 1.0 / sqrt(nsq > 1.0 ? nsq : 1.0);  // nsq <= 1: f == 1.0 exactly
+#pragma unroll
+    for (int j = 0; j < C; ++j) x[j] *= f;
+}
+
+// FTL action (fast_algorithms.py:37-49): x = -(1/||theta||) * theta, or 0
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ void ocx_action_ftl(const double (&th)[C], double (&x)[C], int lane) {
+    double p[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+    const double nsq = ocx_total<C, P, CHAIN>(p, lane);
+    const double sc = -(1.0 / sqrt(nsq));
+#pragma unroll
+    for (int j = 0; j < C; ++j) x[j] = (nsq == 0.0) ? 0.0 : sc * th[j];
+}
+
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
+    double p[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * x[j];
+    return ocx_total<C, P, CHAIN>(p, lane);
+}
+
+// ---------------------------------------------------------------------------
+// fast_algorithms.py:88-115 `_simulate_alg_core` (+ exact_ftl.py:230-277 outputs)
+// ---------------------------------------------------------------------------
+template <int C, int P, bool CHAIN, int NB>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t d, int64_t G, int alg_flag, double eta0, const double* __restrict__ comparator,
+    double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
+    double* __restrict__ x_last) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 32 * C;  // ocx_d2 per step tile
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const double* __restrict__ yp = yt + g * T * S + s;
+    const bool ftl = (alg_flag != 0);
+
+    double th[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = 0.0;
+
+    ocx_d2 zb[NB][K];
+    double yb[NB];
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            yb[u] = yp[u * S];
+        }
+
+    double cum = 0.0;
+    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+                const int64_t tp = t + NB - 1;
+                if (tp < T) {
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                    yb[(u + NB - 1) % NB] = yp[tp * S];
+                }
+                double x[C];
+                if (!ftl) ocx_action_ftrl<C, P, CHAIN>(th, t + 1, eta0, x, lane);
+                else ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                const double q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);  // :105
+                if (x_last != nullptr && t == T - 1 && b < B) {
+#pragma unroll
+                    for (int j = 0; j < C; ++j) {
+                        const int64_t jj = (int64_t)c * C + j;
+                        if (jj < d) x_last[b * d + jj] = x[j];
+                    }
+                }
+                const double diff = q - yb[u];  // :106-111
+                cum += 0.5 * fabs(diff);
+                const double gq = ocx_grad(diff);
+#pragma unroll
+                for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);  // gq*z is exact
+            }
+        }
+    }
+
+    // ---- comparator action (fast_algorithms.py:113 FTL of theta, or the caller's) ----
+    double xs[C];
+    if (comparator != nullptr) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            const int64_t jj = (int64_t)c * C + j;
+            xs[j] = (b < B && jj < d) ? comparator[b * d + jj] : 0.0;
+        }
+    } else {
+        ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
+    }
+
+    // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            yb[u] = yp[u * S];
+        }
+    double comp = 0.0;
+    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+                const int64_t tp = t + NB - 1;
+                if (tp < T) {
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                    yb[(u + NB - 1) % NB] = yp[tp * S];
+                }
+                const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                comp += 0.5 * fabs(q - yb[u]);
+            }
+        }
+    }
+
+    if (c == 0 && b < B) {
+        if (regret) regret[b] = cum - comp;
+        if (cum_out) cum_out[b] = cum;
+        if (comp_out) comp_out[b] = comp;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fast_algorithms.py:118-164 `_simulate_SMART_like_core`
+// ---------------------------------------------------------------------------
+template <int C, int P, bool CHAIN>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t G, const double* __restrict__ thresh, double eta0, double* __restrict__ regret,
+    int64_t* __restrict__ switch_step) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 32 * C;
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const double* __restrict__ yp = yt + g * T * S + s;
+    const double th_sw = (b < B) ? thresh[b] : 0.0;
+
+    double tf[C], tr[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) tf[j] = tr[j] = 0.0;
+    bool switched = (b >= B);  // padding sequences never scan
+    int64_t sw = -1;
+    double ftl_loss = 0.0, total_loss = 0.0;
+
+    for (int64_t t = 0; t < T; ++t) {
+        ocx_d2 z[K];
+        ocx_load_tile<C>(z, zp + t * tstride);
+        const double yv = yp[t * S];
+        // FTL is always run and updated (:140-146)
+        double x[C];
+        ocx_action_ftl<C, P, CHAIN>(tf, x, lane);
+        const double pf = ocx_zdot<C, P, CHAIN>(z, x, lane);
+        const double dfl = pf - yv;
+        const double gfl = ocx_grad(dfl);
+#pragma unroll
+        for (int j = 0; j < C; ++j) tf[j] += gfl * ocx_zj(z, j);
+        const double loss_ftl = 0.5 * fabs(dfl);
+        ftl_loss += loss_ftl;
+        if (switched) {
+            // post-switch: FTRL with its own theta and the global t (:148-154)
+            ocx_action_ftrl<C, P, CHAIN>(tr, t + 1, eta0, x, lane);
+            const double pr = ocx_zdot<C, P, CHAIN>(z, x, lane);
+            const double dr = pr - yv;
+            total_loss += 0.5 * fabs(dr);
+            const double gr = ocx_grad(dr);
+#pragma unroll
+            for (int j = 0; j < C; ++j) tr[j] += gr * ocx_zj(z, j);
+        } else {
+            total_loss += loss_ftl;  // :156
+            // s_t = FTL(theta_ftl) after the update; loss of s_t over rows 0..t (:157-160)
+            double sv[C];
+            ocx_action_ftl<C, P, CHAIN>(tf, sv, lane);
+            double s_loss = 0.0;
+            for (int64_t i = 0; i <= t; ++i) {
+                ocx_d2 zi[K];
+                ocx_load_tile<C>(zi, zp + i * tstride);
+                const double q = ocx_zdot<C, P, CHAIN>(zi, sv, lane);
+                s_loss += 0.5 * fabs(q - yp[i * S]);
+            }
+            if (ftl_loss - s_loss >= th_sw) {
+                switched = true;
+                sw = t;
+            }
+        }
+    }
+    // final comparator = FTL(theta_ftl) (:162-163)
+    double sv[C];
+    ocx_action_ftl<C, P, CHAIN>(tf, sv, lane);
+    double comp = 0.0;
+    for (int64_t t = 0; t < T; ++t) {
+        ocx_d2 z[K];
+        ocx_load_tile<C>(z, zp + t * tstride);
+        const double q = ocx_zdot<C, P, CHAIN>(z, sv, lane);
+        comp += 0.5 * fabs(q - yp[t * S]);
+    }
+    if (c == 0 && b < B) {
+        regret[b] = total_loss - comp;
+        if (switch_step) switch_step[b] = sw;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// exact_ftl.py:306-333 `replay_exact_ftl`: loss of given actions a_t, comparator a_T
+// ---------------------------------------------------------------------------
+template <int C, int P, bool CHAIN>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, const double* __restrict__ at,
+    int64_t B, int64_t T, int64_t G, double* __restrict__ cum_out, double* __restrict__ comp_out) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 32 * C;
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const ocx_d2* __restrict__ ap =
+        reinterpret_cast<const ocx_d2*>(at) + g * (T + 1) * tstride + lane;
+    const double* __restrict__ yp = yt + g * T * S + s;
+    double aT[C];
+    {
+        ocx_d2 a2[K];
+        ocx_load_tile<C>(a2, ap + T * tstride);
+#pragma unroll
+        for (int j = 0; j < C; ++j) aT[j] = ocx_zj(a2, j);
+    }
+    double cum = 0.0, comp = 0.0;
+    for (int64_t t = 0; t < T; ++t) {
+        ocx_d2 z[K], a2[K];
+        ocx_load_tile<C>(z, zp + t * tstride);
+        ocx_load_tile<C>(a2, ap + t * tstride);
+        const double yv = yp[t * S];
+        double a[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) a[j] = ocx_zj(a2, j);
+        const double q = ocx_zdot<C, P, CHAIN>(z, a, lane);
+        const double qc = ocx_zdot<C, P, CHAIN>(z, aT, lane);
+        cum += 0.5 * fabs(q - yv);
+        comp += 0.5 * fabs(qc - yv);
+    }
+    if (c == 0 && b < B) {
+        cum_out[b] = cum;
+        comp_out[b] = comp;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Layout packing and small reductions
+// ---------------------------------------------------------------------------
+__global__ void ocx_pack_z_kernel(const double* __restrict__ z, double* __restrict__ zt,
+                                  int64_t B, int64_t T, int64_t d, int P, int C, int64_t total) {
+    const int S = 64 / P;
+    const int64_t tile = 64 * (int64_t)C;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t tix = o / tile;
+        const int r = (int)(o - tix * tile);
+        const int k = r >> 7, L = (r & 127) >> 1, e = r & 1;
+        const int64_t g = tix / T, t = tix - (tix / T) * T;
+        const int64_t b = g * S + L / P;
+        const int64_t j = (int64_t)(L % P) * C + 2 * k + e;
+        zt[o] = (b < B && j < d) ? z[(b * T + t) * d + j] : 0.0;
+    }
+}
+
+__global__ void ocx_pack_y_kernel(const double* __restrict__ y, double* __restrict__ ytl,
+                                  int64_t B, int64_t T, int S, int64_t total) {
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t tix = o / S;
+        const int s = (int)(o - tix * S);
+        const int64_t g = tix / T, t = tix - (tix / T) * T;
+        const int64_t b = g * S + s;
+        ytl[o] = (b < B) ? y[b * T + t] : 0.0;
+    }
+}
+
+// max over runs starting from 0.0 with `reg > max` (fast_algorithms.py:228, :242-243)
+__global__ void ocx_max_kernel(const double* __restrict__ r, int64_t B, double* __restrict__ out) {
+    __shared__ double sm[OCX_BLOCK];
+    double m = 0.0;
+    for (int64_t i = threadIdx.x; i < B; i += blockDim.x) {
+        const double v = r[i];
+        if (v > m) m = v;
+    }
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = OCX_BLOCK / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w && sm[threadIdx.x + w] > sm[threadIdx.x])
+            sm[threadIdx.x] = sm[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = sm[0];
+}
+
+// ---------------------------------------------------------------------------
+// Launchers: runtime (C, P) → template instance
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int nb_for(int C) { return C <= 8 ? 4 : (C <= 16 ? 3 : 2); }
+
+inline unsigned grid_for(int64_t G) {
+    return (unsigned)((G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK);
+}
+
+template <int C, int P, bool CH>
+hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+                         double eta0, const double* cmp, double* reg, double* cum, double* comp,
+                         double* xl, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C)>), dim3(grid_for(L->G)),
+                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, alg_flag, eta0,
+                       cmp, reg, cum, comp, xl);
+    return hipGetLastError();
+}
+
+template <int C, int P, bool CH>
+hipError_t launch_smart_cp(const ocx_layout* L, const double* zt, const double* yt,
+                           const double* th, double eta0, double* reg, int64_t* sw,
+                           hipStream_t st) {
+    hipLaunchKernelGGL((ocx_smart_kernel<C, P, CH>), dim3(grid_for(L->G)), dim3(OCX_BLOCK), 0, st,
+                       zt, yt, L->B, L->T, L->G, th, eta0, reg, sw);
+    return hipGetLastError();
+}
+
+template <int C, int P, bool CH>
+hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double* yt,
+                            const double* at, double* cum, double* comp, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_replay_kernel<C, P, CH>), dim3(grid_for(L->G)), dim3(OCX_BLOCK), 0,
+                       st, zt, yt, at, L->B, L->T, L->G, cum, comp);
+    return hipGetLastError();
+}
+
+// (C, P) tree instances for every supported C; chain (exact mode, d > 64) uses C = 64.
+#define OCX_DISPATCH_P(FN, C, ...)                    \
+    switch (L->P) {                                   \
+        case 1: return FN<C, 1, false>(__VA_ARGS__);  \
+        case 2: return FN<C, 2, false>(__VA_ARGS__);  \
+        case 4: return FN<C, 4, false>(__VA_ARGS__);  \
+        case 8: return FN<C, 8, false>(__VA_ARGS__);  \
+        case 16: return FN<C, 16, false>(__VA_ARGS__); \
+        case 32: return FN<C, 32, false>(__VA_ARGS__); \
+        case 64: return FN<C, 64, false>(__VA_ARGS__); \
+        default: return hipErrorInvalidValue;         \
+    }
+
+#define OCX_DISPATCH(FN, ...)                                         \
+    if (L->chain) {                                                   \
+        if (L->C != 64) return hipErrorInvalidValue;                  \
+        switch (L->P) {                                               \
+            case 2: return FN<64, 2, true>(__VA_ARGS__);              \
+            case 4: return FN<64, 4, true>(__VA_ARGS__);              \
+            case 8: return FN<64, 8, true>(__VA_ARGS__);              \
+            case 16: return FN<64, 16, true>(__VA_ARGS__);            \
+            case 32: return FN<64, 32, true>(__VA_ARGS__);            \
+            case 64: return FN<64, 64, true>(__VA_ARGS__);            \
+            default: return hipErrorInvalidValue;                     \
+        }                                                             \
+    }                                                                 \
+    switch (L->C) {                                                   \
+        case 2: OCX_DISPATCH_P(FN, 2, __VA_ARGS__)                    \
+        case 4: OCX_DISPATCH_P(FN, 4, __VA_ARGS__)                    \
+        case 6: OCX_DISPATCH_P(FN, 6, __VA_ARGS__)                    \
+        case 8: OCX_DISPATCH_P(FN, 8, __VA_ARGS__)                    \
+        case 12: OCX_DISPATCH_P(FN, 12, __VA_ARGS__)                  \
+        case 16: OCX_DISPATCH_P(FN, 16, __VA_ARGS__)                  \
+        case 24: OCX_DISPATCH_P(FN, 24, __VA_ARGS__)                  \
+        case 32: OCX_DISPATCH_P(FN, 32, __VA_ARGS__)                  \
+        case 48: OCX_DISPATCH_P(FN, 48, __VA_ARGS__)                  \
+        case 64: OCX_DISPATCH_P(FN, 64, __VA_ARGS__)                  \
+        default: return hipErrorInvalidValue;                         \
+    }
+}  // namespace
+
+bool ocx_supported_C(int C) {
+    return C == 2 || C == 4 || C == 6 || C == 8 || C == 12 || C == 16 || C == 24 || C == 32 ||
+           C == 48 || C == 64;
+}
+
+hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
+                          double* xl, hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    OCX_DISPATCH(launch_alg_cp, L, zt, yt, alg_flag, eta0, cmp, reg, cum, comp, xl, st)
+}
+
+hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
+                            const double* th, double eta0, double* reg, int64_t* sw,
+                            hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    OCX_DISPATCH(launch_smart_cp, L, zt, yt, th, eta0, reg, sw, st)
+}
+
+hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double* yt,
+                             const double* at, double* cum, double* comp, hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    OCX_DISPATCH(launch_replay_cp, L, zt, yt, at, cum, comp, st)
+}
+hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
+                           double* ytl, hipStream_t st) {
+    const int64_t zn = L->z_elems, yn = L->y_elems;
+    if (zn > 0) {
+        const unsigned grid = (unsigned)std::min<int64_t>((zn + 255) / 256, 65536);
+        hipLaunchKernelGGL(ocx_pack_z_kernel, dim3(grid), dim3(256), 0, st, z, zt, L->B, L->T,
+                           L->d, L->P, L->C, zn);
+    }
+    if (yn > 0) {
+        const unsigned grid = (unsigned)std::min<int64_t>((yn + 255) / 256, 65536);
+        hipLaunchKernelGGL(ocx_pack_y_kernel, dim3(grid), dim3(256), 0, st, y, ytl, L->B, L->T,
+                           L->S, yn);
+    }
+    return hipGetLastError();
+}
+
+hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(ocx_max_kernel, dim3(1), dim3(OCX_BLOCK), 0, st, r, B, out);
+    return hipGetLastError();
+}

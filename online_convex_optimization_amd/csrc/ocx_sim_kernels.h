@@ -1,0 +1,21 @@
+// ocx_sim_kernels.h — host-side launchers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ocx.h"
+
+bool ocx_supported_C(int C);
+hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
+                          double* xl, hipStream_t st);
+hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
+                            const double* th, double eta0, double* reg, int64_t* sw,
+                            hipStream_t st);
+hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double* yt,
+                             const double* at, double* cum, double* comp, hipStream_t st);
+hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
+                           double* ytl, hipStream_t st);
+hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
+hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
+                             double* ytl, hipStream_t st);

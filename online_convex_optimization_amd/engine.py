@@ -1,0 +1,228 @@
+"""Batched API of the MI355X engine (new surface; the reference has only scalar calls).
+
+Two ways in:
+
+* host arrays (numpy) — ``simulate_alg_batch``, ``simulate_smart_batch``,
+  ``replay_batch``, ``gT_regrets``: one synchronous call per batch, results back
+  as numpy;
+* device-resident batches — ``DeviceBatch``: z/y live in HBM in the engine's tiled
+  layout (``include/ocx.h``), generated on device or packed once, then simulated
+  any number of times without touching the host.  Device memory and streams come
+  from PyTorch (plumbing only); every kernel is the HIP code in ``csrc/``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import ptr
+
+SQRT2 = math.sqrt(2.0)
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _check_zy(z: np.ndarray, y: np.ndarray):
+    if z.ndim != 3:
+        raise ValueError(f"z must be [B, T, d], got shape {z.shape}")
+    B, T, d = z.shape
+    if y.shape != (B, T):
+        raise ValueError(f"y must be [B, T] = {(B, T)}, got {y.shape}")
+    return B, T, d
+
+
+def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=None, *,
+                       lanes_per_seq: int = 0, device: int = 0, return_all: bool = False):
+    """fast_algorithms.py:88-115 over B independent sequences on one GPU.
+
+    z [B, T, d], y [B, T]; comparator [B, d] optional (exact_ftl.py:266-269).
+    Returns regret [B] or, with ``return_all``, (regret, cum_loss, comp_loss, x_last)."""
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    cmp = None
+    if comparator is not None:
+        cmp = _f64(comparator)
+        if cmp.shape != (B, d):
+            raise ValueError(f"comparator must be [B, d] = {(B, d)}, got {cmp.shape}")
+    reg = np.zeros(B)
+    cum = np.zeros(B) if return_all else None
+    comp = np.zeros(B) if return_all else None
+    xl = np.zeros((B, d)) if return_all else None
+    _lib.call("ocx_simulate_alg_batch", ptr(z), ptr(y), B, T, d, int(alg_flag), float(eta0),
+              ptr(cmp), ptr(reg), ptr(cum), ptr(comp), ptr(xl), int(lanes_per_seq), int(device))
+    if return_all:
+        return reg, cum, comp, xl
+    return reg
+
+
+def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = 0,
+                         device: int = 0, return_switch: bool = False):
+    """fast_algorithms.py:118-164 over B sequences; thresh scalar or [B]."""
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    th = _f64(np.broadcast_to(np.asarray(thresh, dtype=np.float64), (B,)))
+    reg = np.zeros(B)
+    sw = np.zeros(B, dtype=np.int64)
+    _lib.call("ocx_simulate_smart_batch", ptr(z), ptr(y), B, T, d, ptr(th), float(eta0), ptr(reg),
+              sw.ctypes.data_as(_lib.c_i64p), int(lanes_per_seq), int(device))
+    return (reg, sw) if return_switch else reg
+
+
+def replay_batch(z, y, actions, *, device: int = 0):
+    """exact_ftl.py:306-333 over B sequences: actions [B, T+1, d] → (cum_loss, comp_loss)."""
+    z = _f64(z)
+    y = _f64(y)
+    a = _f64(actions)
+    B, T, d = _check_zy(z, y)
+    if a.shape != (B, T + 1, d):
+        raise ValueError(f"actions must be [B, T+1, d] = {(B, T + 1, d)}, got {a.shape}")
+    cum = np.zeros(B)
+    comp = np.zeros(B)
+    _lib.call("ocx_replay_batch", ptr(z), ptr(y), ptr(a), B, T, d, ptr(cum), ptr(comp),
+              int(device))
+    return cum, comp
+
+
+def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
+               run0: int = 0, lanes_per_seq: int = 0, device: int = 0) -> np.ndarray:
+    """Regrets of FTRL on _rng(base_seed, T, run) sequences, run in [run0, run0+runs),
+    generated on device (fast_algorithms.py:230-241 with a ``d`` parameter)."""
+    if base_seed < 0 or base_seed >= 2 ** 64:
+        raise ValueError("base_seed must be in [0, 2**64)")
+    out = np.zeros(int(runs))
+    _lib.call("ocx_gT_regrets", int(base_seed), int(T), int(run0), int(runs), int(d),
+              float(eta0), ptr(out), int(lanes_per_seq), int(device))
+    return out
+
+
+def max_regret(regrets: np.ndarray) -> float:
+    """fast_algorithms.py:228, :242-243 — max over runs starting from 0.0 (`reg > max`)."""
+    r = np.asarray(regrets, dtype=np.float64)
+    pos = r[r > 0.0]
+    return float(pos.max()) if pos.size else 0.0
+
+
+def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
+             eta0: float = SQRT2, devices: Optional[Sequence[int]] = None,
+             lanes_per_seq: int = 0) -> dict:
+    """empirical_worst_case_thresholds on one or several GPUs of this process.
+
+    Runs are split into contiguous shards, one per device, each generated and
+    simulated on its own GPU (threads: ctypes releases the GIL); the per-shard
+    regrets are concatenated in run order.  Returns {T: (g(T), regrets[runs])}."""
+    devs = list(devices) if devices else [0]
+    out = {}
+    for T in T_grid:
+        T = int(T)
+        bounds = np.linspace(0, runs, len(devs) + 1).astype(np.int64)
+        parts = [None] * len(devs)
+
+        def work(i):
+            lo, hi = int(bounds[i]), int(bounds[i + 1])
+            parts[i] = gT_regrets(T, hi - lo, base_seed=base_seed, d=d, eta0=eta0, run0=lo,
+                                  lanes_per_seq=lanes_per_seq, device=devs[i])
+
+        if len(devs) == 1:
+            work(0)
+        else:
+            import concurrent.futures as cf
+            with cf.ThreadPoolExecutor(len(devs)) as ex:
+                list(ex.map(work, range(len(devs))))
+        regs = np.concatenate(parts)
+        out[T] = (max_regret(regs), regs)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Device-resident batches (torch tensors as HBM buffers)
+# ---------------------------------------------------------------------------
+
+class DeviceBatch:
+    """B sequences of T steps in d dimensions, resident in HBM in the tiled layout.
+
+    ``stream`` is a torch.cuda.Stream (default: the current stream); every kernel
+    of this object is launched on it, so torch events recorded on that stream
+    bracket the HIP kernels exactly."""
+
+    def __init__(self, B: int, T: int, d: int, *, lanes_per_seq: int = 0, device: int = 0,
+                 stream=None):
+        import torch
+        self.torch = torch
+        self.L = _lib.layout(B, T, d, lanes_per_seq)
+        self.device = torch.device("cuda", device)
+        with torch.cuda.device(self.device):
+            self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+            self.z = torch.empty(max(self.L.z_elems, 1), dtype=torch.float64, device=self.device)
+            self.y = torch.empty(max(self.L.y_elems, 1), dtype=torch.float64, device=self.device)
+            self.regret = torch.zeros(max(B, 1), dtype=torch.float64, device=self.device)
+            self.cum = torch.zeros_like(self.regret)
+            self.comp = torch.zeros_like(self.regret)
+
+    @property
+    def _sp(self):
+        return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _lp(self):
+        return ctypes.byref(self.L)
+
+    def generate_gT(self, base_seed: int = 0, run0: int = 0):
+        """Fill z/y with _rng(base_seed, T, run0 + b) sequences (on device)."""
+        _lib.call("ocx_dev_gen_gT", self._lp(), int(base_seed), int(run0), self.z.data_ptr(),
+                  self.y.data_ptr(), self._sp)
+        return self
+
+    def pack(self, z, y):
+        """Copy host/device arrays z [B,T,d], y [B,T] into the tiled layout."""
+        torch = self.torch
+        zt = torch.as_tensor(np.ascontiguousarray(z, dtype=np.float64) if isinstance(z, np.ndarray)
+                             else z).to(self.device, torch.float64).contiguous()
+        yt = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float64) if isinstance(y, np.ndarray)
+                             else y).to(self.device, torch.float64).contiguous()
+        if tuple(zt.shape) != (self.L.B, self.L.T, self.L.d) or tuple(yt.shape) != (self.L.B, self.L.T):
+            raise ValueError("z/y shape does not match the batch")
+        _lib.call("ocx_dev_pack", self._lp(), zt.data_ptr(), yt.data_ptr(), self.z.data_ptr(),
+                  self.y.data_ptr(), self._sp)
+        self._keep = (zt, yt)
+        return self
+
+    def simulate_alg(self, alg_flag: int = 0, eta0: float = SQRT2, comparator=None,
+                     x_last=None):
+        """Launch the FTRL/FTL kernel; results land in self.regret/cum/comp (async)."""
+        cp = comparator.data_ptr() if comparator is not None else None
+        xp = x_last.data_ptr() if x_last is not None else None
+        _lib.call("ocx_dev_simulate_alg", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+                  int(alg_flag), float(eta0), cp, self.regret.data_ptr(), self.cum.data_ptr(),
+                  self.comp.data_ptr(), xp, self._sp)
+        return self.regret
+
+    def simulate_smart(self, thresh, eta0: float = SQRT2, switch_step=None):
+        th = self.torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
+                                                  (self.L.B,)).copy()).to(self.device)
+        sp = switch_step.data_ptr() if switch_step is not None else None
+        _lib.call("ocx_dev_simulate_smart", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+                  th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, self._sp)
+        self._keep_th = th
+        return self.regret
+
+    def max_regret(self, out=None):
+        torch = self.torch
+        out = out if out is not None else torch.zeros(1, dtype=torch.float64, device=self.device)
+        _lib.call("ocx_dev_max_regret", self.regret.data_ptr(), int(self.L.B), out.data_ptr(),
+                  self._sp)
+        return out
+
+    @property
+    def z_bytes(self) -> int:
+        return int(self.L.z_elems) * 8
+
+    @property
+    def y_bytes(self) -> int:
+        return int(self.L.y_elems) * 8

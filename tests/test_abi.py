@@ -1,0 +1,91 @@
+"""CPU checks of the C ABI: libocx.so loads, exports every symbol include/ocx.h declares,
+the ctypes binding covers them, and layout planning (pure host logic) is right."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from online_convex_optimization_amd import _lib
+from tests._tiles import untile_y, untile_z
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "ocx.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*int\s+(ocx_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (ocx_\w+)$", out, flags=re.M))
+    assert set(syms) <= exported
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+
+
+def test_version_and_error_channel():
+    assert _lib.load().ocx_version() == 100
+    with pytest.raises(ValueError):
+        _lib.layout(-1, 10, 5)
+    assert "negative" in _lib.last_error()
+
+
+@pytest.mark.parametrize("B,T,d,P", [(1, 1000, 5, 1), (32768, 10000, 64, 0), (65536, 1000, 16, 0),
+                                     (2048, 10, 1024, 0), (100, 7, 3, 4), (5, 3, 0, 0)])
+def test_layout(B, T, d, P):
+    L = _lib.layout(B, T, d, P)
+    assert L.P * L.S == 64 and L.C % 2 == 0 and L.Dp == L.P * L.C >= d
+    assert L.G == -(-B // L.S)
+    assert L.z_elems == L.G * T * 64 * L.C and L.y_elems == L.G * T * L.S
+    if P:
+        assert L.P == P
+
+
+def test_auto_layout_choices():
+    assert (_lib.layout(32768, 10, 64).P, _lib.layout(32768, 10, 64).C) == (4, 16)
+    assert _lib.layout(1 << 20, 10, 64).P == 1          # enough sequences: exact mode
+    assert _lib.layout(1, 10, 5).C == 2                 # lanes keep >= 2 coordinates
+    assert _lib.layout(8, 10, 4096).C == 64             # d/P <= 64
+    with pytest.raises(_lib.OCXError):
+        _lib.layout(1, 10, 5000)
+    ex = _lib.layout(3, 10, 1000, 1)                     # exact mode above 64 coordinates
+    assert (ex.P, ex.C, ex.chain) == (16, 64, 1)
+    assert _lib.layout(3, 10, 64, 1).chain == 0
+
+
+def test_untile_roundtrip_matches_pack_formula():
+    # host restatement of ocx_pack_z_kernel's index map, inverted by untile_z
+    B, T, d = 37, 5, 11
+    for P in (1, 2, 4, 8, 64):
+        L = _lib.layout(B, T, d, P)
+        rng = np.random.default_rng(P)
+        z = rng.standard_normal((B, T, d))
+        y = rng.standard_normal((B, T))
+        zt = np.zeros(L.z_elems)
+        o = np.arange(L.z_elems)
+        tile = 64 * L.C
+        tix, r = o // tile, o % tile
+        k, lane, e = r >> 7, (r & 127) >> 1, r & 1
+        g, t = tix // T, tix % T
+        b = g * L.S + lane // L.P
+        j = (lane % L.P) * L.C + 2 * k + e
+        ok = (b < B) & (j < d)
+        zt[ok] = z[b[ok], t[ok], j[ok]]
+        assert np.array_equal(untile_z(zt, L), z)
+        yt = np.zeros(L.y_elems)
+        o = np.arange(L.y_elems)
+        tix, s = o // L.S, o % L.S
+        g, t = tix // T, tix % T
+        b = g * L.S + s
+        ok = b < B
+        yt[ok] = y[b[ok], t[ok]]
+        assert np.array_equal(untile_y(yt, L), y)
