@@ -66,6 +66,23 @@ _lib = None
 _lock = threading.Lock()
 
 
+def _share_torch_hip_runtime() -> None:
+    """Load PyTorch's HIP runtime first when PyTorch is installed.
+
+    torch ships its own libamdhip64 (soname libamdhip64.so.7, NEEDED as the
+    unversioned libamdhip64.so).  libocx NEEDs libamdhip64.so.7: if torch is loaded
+    first, the dynamic loader binds libocx to torch's runtime and the process has ONE
+    HIP runtime, so device pointers and streams from torch tensors are valid in
+    libocx.  Loading libocx first would pull /opt/rocm's runtime and torch would then
+    load a second one and see no GPU."""
+    if os.environ.get("OCX_NO_TORCH"):
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load():
     """Load libocx.so (raises OCXError if it is missing: no fallback exists)."""
     global _lib
@@ -73,6 +90,7 @@ def load():
         return _lib
     with _lock:
         if _lib is None:
+            _share_torch_hip_runtime()
             if not os.path.exists(LIB_PATH):
                 raise OCXError(f"libocx.so not found at {LIB_PATH}: the HIP extension is not "
                                "built (python -m online_convex_optimization_amd._build)")
