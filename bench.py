@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--B", type=int, default=32768, help="sequences per GPU (resident batch)")
     ap.add_argument("--T", type=int, default=10000)
     ap.add_argument("--d", type=int, default=64)
-    ap.add_argument("--lanes", type=int, default=0, help="lanes per sequence (0 = auto)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="lanes_per_seq (include/ocx.h): 1 = exact mode (bit-identical to the "
+                         "reference, auto lanes), 0 = auto with butterfly sums, k / -k explicit")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -164,7 +166,10 @@ def main():
             "config": {"workload": "configs[2]: batched FTRL d=64 T=1e4 (1e5-trial job as "
                                    "resident batches of B per GPU)",
                        "B_per_gpu": B, "T": T, "d": d, "lanes_per_seq": int(db.L.P),
-                       "coords_per_lane": int(db.L.C), "parallelism": f"dp{world}",
+                       "coords_per_lane": int(db.L.C),
+                       "sums": "exact (sequential order)" if (a.lanes == 1 or a.lanes < 0)
+                               else "butterfly",
+                       "parallelism": f"dp{world}",
                        "z_bytes_per_gpu": db.z_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

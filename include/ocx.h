@@ -19,12 +19,14 @@
  *     (see ocx_layout) and a hipStream_t passed as void* (NULL = default stream);
  *     they are asynchronous and capture-safe (no allocation, no sync).
  *   - All arithmetic is IEEE binary64 (dtype "f64").
- *   - lanes_per_seq: 1 = "exact" (every sum in the reference's sequential order →
- *     bit-identical results; one lane per sequence for d <= 64, above that the
- *     running sum is handed from lane to lane, layout.chain = 1); 2..64 (power of 2) =
- *     a sequence's coordinates split over that many lanes of one wavefront
- *     (butterfly reductions; ~1e-16 relative to the reference); 0 = auto
- *     (throughput: picks P from B and d).
+ *   - lanes_per_seq selects how a sequence's d coordinates map onto lanes:
+ *       0      auto: the fewest lanes that fill the GPU; partial sums combined by a
+ *              butterfly (~1e-16 relative to the reference's sequential sums);
+ *       k >= 2 k lanes (power of two), butterfly sums;
+ *       1      exact, auto lanes (<= 4 unless d needs more): every sum in the
+ *              reference's sequential order, so results are bit-identical;
+ *       -k     exact with k lanes; for k > 1 the running sum is handed from lane to
+ *              lane (layout.chain = 1).
  */
 #ifndef OCX_H_
 #define OCX_H_

@@ -72,6 +72,25 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
     return LIB
 
 
+def build_variant(name: str, defines, jobs: int = 4) -> str:
+    """Tuning variant: ocx_sim.hip recompiled with -D overrides, linked into
+    tune_build/libocx_<name>.so (never loaded by the product path)."""
+    hipcc = _hipcc()
+    out_dir = os.path.join(ROOT, "tune_build")
+    os.makedirs(out_dir, exist_ok=True)
+    build(jobs=jobs)  # the shared objects of the other sources
+    obj = os.path.join(out_dir, f"ocx_sim_{name}.o")
+    lib = os.path.join(out_dir, f"libocx_{name}.so")
+    dflags = [f"-D{d}" for d in defines]
+    src = os.path.join(CSRC, "ocx_sim.hip")
+    if _stale(lib, [src, *[os.path.join(CSRC, h) for h in HEADERS]]):
+        subprocess.run([hipcc, *CFLAGS, *dflags, "-c", src, "-o", obj], check=True)
+        others = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES if s != "ocx_sim.hip"]
+        subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", obj, *others, "-o", lib],
+                       check=True)
+    return lib
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")

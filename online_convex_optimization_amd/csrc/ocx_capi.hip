@@ -116,36 +116,38 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     if (!L) return fail(OCX_E_INVALID, "layout is NULL");
     if (B < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative size");
     if (d > 4096) return fail(OCX_E_UNSUPPORTED, "d > 4096 not supported");
-    int P = lanes_per_seq;
-    if (P == 0) {
-        // auto: the fewest lanes per sequence that still gives
-        // ~8 wavefronts per CU (131072 lanes on 256 CUs), clamped so a lane keeps
-        // >= 2 coordinates (no lane of pure padding) and <= 64 coordinates.
+    // lanes_per_seq: 0 = auto (tree sums), k >= 2 = k lanes (tree sums),
+    // 1 = exact with auto lanes, -k = exact with k lanes.  Exact mode keeps every sum
+    // in the reference's sequential order; with P > 1 the running sum is handed from
+    // lane to lane (chain = 1).
+    const bool exact = (lanes_per_seq == 1 || lanes_per_seq < 0);
+    int P = lanes_per_seq < 0 ? -lanes_per_seq : lanes_per_seq;
+    // fewest lanes with <= 64 coordinates each; most lanes keeping >= 2 coordinates
+    int64_t p_min = 1;
+    while (p_min < 64 && ceil_div(d, p_min) > 64) p_min *= 2;
+    int64_t p_max = 1;
+    while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
+    if (lanes_per_seq == 0 || lanes_per_seq == 1) {
+        // auto: enough lanes for ~8 wavefronts per CU (131072 lanes on
+        // 256 CUs) when B allows; exact mode caps the chain at 4 lanes.
         int64_t p_lanes = 1;
         while (p_lanes < 64 && p_lanes * B < 131072) p_lanes *= 2;
-        int64_t p_min = 1;
-        while (p_min < 64 && ceil_div(d, p_min) > 64) p_min *= 2;
-        int64_t p_max = 1;
-        while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
-        P = (int)std::max(p_min, std::min(p_lanes, p_max));
+        int64_t hi = exact ? std::min<int64_t>(p_max, 4) : p_max;
+        P = (int)std::max(p_min, std::min(p_lanes, std::max<int64_t>(hi, 1)));
     }
     if (P < 1 || P > 64 || (P & (P - 1)) != 0)
-        return fail(OCX_E_INVALID, "lanes_per_seq must be 0 or a power of two in [1, 64]");
-    int chain = 0;
+        return fail(OCX_E_INVALID, "lanes_per_seq must be 0, 1, or +/- a power of two <= 64");
+    const int chain = (exact && P > 1) ? 1 : 0;
     int C;
-    if (P == 1 && d > 64) {
-        // exact mode above 64 coordinates: 64 per lane, running sum handed lane to lane
-        int64_t p = 2;
-        while (p < 64 && ceil_div(d, p) > 64) p *= 2;
-        if (ceil_div(d, p) > 64) return fail(OCX_E_UNSUPPORTED, "d too large for exact mode");
-        P = (int)p;
-        C = 64;
-        chain = 1;
+    const int64_t need = std::max<int64_t>(ceil_div(d, P), 1);
+    if (need > 64)
+        return fail(OCX_E_UNSUPPORTED,
+                    "d / lanes_per_seq > 64 coordinates per lane; use more lanes");
+    if (chain) {
+        C = 2;
+        while (C < need) C *= 2;
     } else {
-        C = even_supported_C(std::max<int64_t>(ceil_div(d, P), 1));
-        if (C < 0)
-            return fail(OCX_E_UNSUPPORTED,
-                        "d / lanes_per_seq > 64 coordinates per lane; use more lanes");
+        C = even_supported_C(need);
     }
     std::memset(L, 0, sizeof(*L));
     L->B = B;
@@ -167,7 +169,8 @@ static int check_layout(const ocx_layout* L) {
     if (!L) return fail(OCX_E_INVALID, "layout is NULL");
     if (!ocx_supported_C(L->C) || L->P < 1 || L->P > 64 || L->S * L->P != 64)
         return fail(OCX_E_INVALID, "corrupt layout");
-    if (L->chain && L->C != 64) return fail(OCX_E_INVALID, "corrupt layout (chain needs C=64)");
+    if (L->chain && (L->C & (L->C - 1)) != 0)
+        return fail(OCX_E_INVALID, "corrupt layout (chain needs a power-of-two C)");
     return OCX_OK;
 }
 

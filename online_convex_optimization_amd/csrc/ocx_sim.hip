@@ -22,7 +22,13 @@ namespace {
 template <int C>
 __device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p) {
 #pragma unroll
-    for (int k = 0; k < C / 2; ++k) dst[k] = __builtin_nontemporal_load(p + k * 64);
+    for (int k = 0; k < C / 2; ++k) {
+#if OCX_LOAD_NT
+        dst[k] = __builtin_nontemporal_load(p + k * 64);
+#else
+        dst[k] = p[k * 64];
+#endif
+    }
 }
 
 __device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
@@ -394,8 +400,23 @@ __global__ void ocx_max_kernel(const double* __restrict__ r, int64_t B, double* 
 // ---------------------------------------------------------------------------
 // Launchers: runtime (C, P) → template instance
 // ---------------------------------------------------------------------------
+// Register-ring depth (steps in flight per wave) by coordinates per lane; tuned on
+// MI355X with tools/tune.py (the -D overrides build the tuning variants).
+#ifndef OCX_NB_LE8
+#define OCX_NB_LE8 4
+#endif
+#ifndef OCX_NB_16
+#define OCX_NB_16 3
+#endif
+#ifndef OCX_NB_GE32
+#define OCX_NB_GE32 2
+#endif
+#ifndef OCX_LOAD_NT
+#define OCX_LOAD_NT 1
+#endif
+
 namespace {
-constexpr int nb_for(int C) { return C <= 8 ? 4 : (C <= 16 ? 3 : 2); }
+constexpr int nb_for(int C) { return C <= 8 ? OCX_NB_LE8 : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32); }
 
 inline unsigned grid_for(int64_t G) {
     return (unsigned)((G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK);
@@ -428,7 +449,8 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
     return hipGetLastError();
 }
 
-// (C, P) tree instances for every supported C; chain (exact mode, d > 64) uses C = 64.
+// (C, P) tree instances for every supported C; chain (exact mode, P > 1) instances for
+// power-of-two C.
 #define OCX_DISPATCH_P(FN, C, ...)                    \
     switch (L->P) {                                   \
         case 1: return FN<C, 1, false>(__VA_ARGS__);  \
@@ -441,16 +463,26 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
         default: return hipErrorInvalidValue;         \
     }
 
+#define OCX_DISPATCH_CHAIN_P(FN, C, ...)             \
+    switch (L->P) {                                  \
+        case 2: return FN<C, 2, true>(__VA_ARGS__);  \
+        case 4: return FN<C, 4, true>(__VA_ARGS__);  \
+        case 8: return FN<C, 8, true>(__VA_ARGS__);  \
+        case 16: return FN<C, 16, true>(__VA_ARGS__); \
+        case 32: return FN<C, 32, true>(__VA_ARGS__); \
+        case 64: return FN<C, 64, true>(__VA_ARGS__); \
+        default: return hipErrorInvalidValue;        \
+    }
+
 #define OCX_DISPATCH(FN, ...)                                         \
     if (L->chain) {                                                   \
-        if (L->C != 64) return hipErrorInvalidValue;                  \
-        switch (L->P) {                                               \
-            case 2: return FN<64, 2, true>(__VA_ARGS__);              \
-            case 4: return FN<64, 4, true>(__VA_ARGS__);              \
-            case 8: return FN<64, 8, true>(__VA_ARGS__);              \
-            case 16: return FN<64, 16, true>(__VA_ARGS__);            \
-            case 32: return FN<64, 32, true>(__VA_ARGS__);            \
-            case 64: return FN<64, 64, true>(__VA_ARGS__);            \
+        switch (L->C) {                                               \
+            case 2: OCX_DISPATCH_CHAIN_P(FN, 2, __VA_ARGS__)          \
+            case 4: OCX_DISPATCH_CHAIN_P(FN, 4, __VA_ARGS__)          \
+            case 8: OCX_DISPATCH_CHAIN_P(FN, 8, __VA_ARGS__)          \
+            case 16: OCX_DISPATCH_CHAIN_P(FN, 16, __VA_ARGS__)        \
+            case 32: OCX_DISPATCH_CHAIN_P(FN, 32, __VA_ARGS__)        \
+            case 64: OCX_DISPATCH_CHAIN_P(FN, 64, __VA_ARGS__)        \
             default: return hipErrorInvalidValue;                     \
         }                                                             \
     }                                                                 \

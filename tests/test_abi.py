@@ -40,14 +40,16 @@ def test_version_and_error_channel():
 
 
 @pytest.mark.parametrize("B,T,d,P", [(1, 1000, 5, 1), (32768, 10000, 64, 0), (65536, 1000, 16, 0),
-                                     (2048, 10, 1024, 0), (100, 7, 3, 4), (5, 3, 0, 0)])
+                                     (2048, 10, 1024, 0), (100, 7, 3, 4), (5, 3, 0, 0),
+                                     (7, 3, 100, -2), (9, 4, 64, -1)])
 def test_layout(B, T, d, P):
     L = _lib.layout(B, T, d, P)
     assert L.P * L.S == 64 and L.C % 2 == 0 and L.Dp == L.P * L.C >= d
     assert L.G == -(-B // L.S)
     assert L.z_elems == L.G * T * 64 * L.C and L.y_elems == L.G * T * L.S
-    if P:
-        assert L.P == P
+    if P > 1 or P < 0:
+        assert L.P == abs(P)
+    assert L.chain == (1 if (P == 1 or P < 0) and L.P > 1 else 0)
 
 
 def test_auto_layout_choices():
@@ -59,7 +61,11 @@ def test_auto_layout_choices():
         _lib.layout(1, 10, 5000)
     ex = _lib.layout(3, 10, 1000, 1)                     # exact mode above 64 coordinates
     assert (ex.P, ex.C, ex.chain) == (16, 64, 1)
-    assert _lib.layout(3, 10, 64, 1).chain == 0
+    assert _lib.layout(3, 10, 64, -1).chain == 0          # exact, one lane per sequence
+    ch = _lib.layout(3, 10, 64, 1)                         # exact, auto lanes: chained
+    assert ch.chain == 1 and ch.P == 4 and ch.C == 16
+    assert _lib.layout(3, 10, 5, -4).C == 2 and _lib.layout(3, 10, 5, -4).chain == 1
+    assert _lib.layout(3, 10, 12, -2).C == 8                # chain C is a power of two
 
 
 def test_untile_roundtrip_matches_pack_formula():

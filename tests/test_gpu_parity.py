@@ -95,7 +95,7 @@ def test_families_all_lane_splits_exact(ocx):
         ref = [O.simulate_alg(z, y, f, SQ2) for f in (0, 1)]
         Z = np.repeat(z[None].astype(np.float64), 3, axis=0)
         Y = np.repeat(y[None].astype(np.float64), 3, axis=0)
-        for P in (1, 2, 4, 8, 16, 32, 64):
+        for P in (1, -1, -8, 2, 4, 8, 16, 32, 64):
             for f in (0, 1):
                 got = eng.simulate_alg_batch(Z, Y, f, SQ2, lanes_per_seq=P)
                 assert np.all(got == ref[f]), (P, f, got, ref[f])
@@ -108,10 +108,10 @@ def test_seeded_gT_golden(ocx, golden):
         by.setdefault((rec["base_seed"], rec["T"]), []).append(rec)
     for (seed, T), recs in by.items():
         runs = max(r["run"] for r in recs) + 1
-        for P in (1, 0):
+        for P in (1, -1, -2, 0):
             got = eng.gT_regrets(T, runs, base_seed=seed, d=5, lanes_per_seq=P)
             for r in recs:
-                if P == 1:
+                if P != 0:
                     assert got[r["run"]] == F(r["regret"]), (seed, T, r["run"])
                 else:
                     assert close(got[r["run"]], F(r["regret"])), (seed, T, r["run"])
@@ -135,7 +135,8 @@ def test_published_gT_curve(ocx):
 
 # ------------------------------------------------------------------ generator
 @pytest.mark.parametrize("B,T,d,P", [(70, 50, 5, 1), (33, 20, 64, 4), (5, 8, 1024, 64),
-                                     (40, 9, 129, 0), (3, 11, 2, 0)])
+                                     (40, 9, 129, 0), (3, 11, 2, 0), (9, 6, 64, -1),
+                                     (17, 7, 100, -2)])
 def test_device_generator_matches_numpy(ocx, B, T, d, P):
     import torch
     eng = ocx["engine"]
@@ -166,12 +167,12 @@ def test_batch_all_lane_splits(ocx, T, d):
     for flag, eta0 in ((0, SQ2), (1, SQ2), (0, 0.3)):
         ref = O.simulate_alg_batch(z, y, flag, eta0, nthreads=4)
         refc = O.simulate_alg_batch(z, y, flag, eta0, comparator=cmp, nthreads=4)
-        for P in (1, 2, 4, 8, 16, 32, 64):
-            if P > 1 and -(-d // P) > 64:
+        for P in (1, -1, -2, -4, -16, -64, 2, 4, 8, 16, 32, 64):
+            if P != 1 and -(-d // abs(P)) > 64:
                 continue
             reg, cum, comp, xl = eng.simulate_alg_batch(z, y, flag, eta0, lanes_per_seq=P,
                                                         return_all=True)
-            if P == 1:
+            if P == 1 or P < 0:  # exact modes (P = 1: auto lanes, -k: k chained lanes)
                 assert np.array_equal(reg, ref[0]) and np.array_equal(cum, ref[1])
                 assert np.array_equal(comp, ref[2]) and np.array_equal(xl, ref[3])
             else:
@@ -191,9 +192,9 @@ def test_smart_batch_splits(ocx):
     y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
     th = rng.uniform(-1.0, 6.0, size=B)
     ref, sw = O.simulate_smart_batch(z, y, th, SQ2, nthreads=4)
-    for P in (1, 2, 4, 8, 64):
+    for P in (1, -1, -4, 2, 4, 8, 64):
         got, gsw = eng.simulate_smart_batch(z, y, th, SQ2, lanes_per_seq=P, return_switch=True)
-        if P == 1:
+        if P == 1 or P < 0:
             assert np.array_equal(got, ref) and np.array_equal(gsw, sw)
         else:
             assert close(got, ref), P
@@ -222,7 +223,7 @@ def test_errors_are_loud(ocx):
 
 # ------------------------------------------------------------------ full-size properties
 def test_full_size_properties(ocx):
-    """Bench-sized batch (d=64, T=1e4): determinism, split invariance (P=1 vs auto),
+    """Bench-sized batch (d=64, T=1e4): determinism, split invariance (exact vs auto),
     and a sample of sequences against the oracle on the very same generated inputs."""
     import torch
     eng = ocx["engine"]
