@@ -16,8 +16,10 @@
 
 #if defined(__HIPCC__)
 #define OCX_HD __host__ __device__ __forceinline__
+#define OCX_HD_NOINLINE __host__ __device__ __noinline__
 #else
 #define OCX_HD static inline
+#define OCX_HD_NOINLINE static __attribute__((noinline))
 #include <math.h>
 #endif
 
@@ -153,17 +155,13 @@ OCX_HD void ocx_rng_init3(ocx_pcg64* g, uint64_t w0, uint64_t w1, uint64_t w2) {
 #define OCX_ZIG_NOR_R 3.6541528853610087963519472518
 #define OCX_ZIG_NOR_INV_R 0.27366123732975827203338247596
 
+// Rejection part of the ziggurat (≈0.7 % of draws), continuing NumPy's for(;;) loop
+// from a rejected draw.  Inlined: an out-of-line call would take the PCG state's
+// address and pin it in scratch memory for the whole kernel.
 template <class KiT, class WiT, class FiT>
-OCX_HD double ocx_standard_normal(ocx_pcg64* g, const KiT& ki, const WiT& wi, const FiT& fi) {
+OCX_HD double ocx_standard_normal_slow(ocx_pcg64* g, const KiT& ki, const WiT& wi,
+                                                const FiT& fi, int idx, uint64_t rabs, double x) {
     for (;;) {
-        uint64_t r = ocx_pcg_next64(g);
-        int idx = (int)(r & 0xff);
-        r >>= 8;
-        int sign = (int)(r & 0x1);
-        uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
-        double x = (double)rabs * wi(idx);
-        if (sign & 0x1) x = -x;
-        if (rabs < ki(idx)) return x;
         if (idx == 0) {
             for (;;) {
                 double xx = -OCX_ZIG_NOR_INV_R * log1p(-ocx_pcg_next_double(g));
@@ -175,7 +173,28 @@ OCX_HD double ocx_standard_normal(ocx_pcg64* g, const KiT& ki, const WiT& wi, co
             if (((fi(idx - 1) - fi(idx)) * ocx_pcg_next_double(g) + fi(idx)) < exp(-0.5 * x * x))
                 return x;
         }
+        uint64_t r = ocx_pcg_next64(g);
+        idx = (int)(r & 0xff);
+        r >>= 8;
+        int sign = (int)(r & 0x1);
+        rabs = (r >> 1) & 0x000fffffffffffffULL;
+        x = (double)rabs * wi(idx);
+        if (sign & 0x1) x = -x;
+        if (rabs < ki(idx)) return x;
     }
+}
+
+template <class KiT, class WiT, class FiT>
+OCX_HD double ocx_standard_normal(ocx_pcg64* g, const KiT& ki, const WiT& wi, const FiT& fi) {
+    uint64_t r = ocx_pcg_next64(g);
+    int idx = (int)(r & 0xff);
+    r >>= 8;
+    int sign = (int)(r & 0x1);
+    uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
+    double x = (double)rabs * wi(idx);
+    if (sign & 0x1) x = -x;
+    if (rabs < ki(idx)) return x; /* 99.3% of the time */
+    return ocx_standard_normal_slow(g, ki, wi, fi, idx, rabs, x);
 }
 
 // NumPy pairwise_sum order for a row of n squares (numpy/_core/src/umath/loops_utils.h):
@@ -227,7 +246,7 @@ OCX_HD void ocx_pw_leaf_begin(ocx_pw_leaf* L, int n) {
     L->n8 = n - (n % 8);
 }
 
-OCX_HD void ocx_pw_leaf_add(ocx_pw_leaf* L, double v) {
+OCX_HD void ocx_pw_leaf_add(ocx_pw_leaf* L, double v) {  // host reference form
     if (L->n < 8) {
         L->res += v;
     } else if (L->i < L->n8) {
@@ -239,4 +258,55 @@ OCX_HD void ocx_pw_leaf_add(ocx_pw_leaf* L, double v) {
         L->res += v;
     }
     L->i++;
+}
+
+// One row of the g(T) sampler: draws d normals in order (NumPy's C order), hands each
+// to store(j, v) and returns their sum of squares in NumPy's pairwise order
+// (np.linalg.norm(z, axis=1)**2).  Leaves are consumed 8 values at a time so the
+// eight accumulators have static indices (registers, not scratch).
+template <class NormalFn, class StoreFn>
+OCX_HD double ocx_row_sumsq(int d, const ocx_pw_plan& plan, NormalFn&& normal, StoreFn&& store) {
+    double stack[16];
+    int sp = 0;
+    int j = 0;
+    for (int op = 0; op < plan.nops; ++op) {
+        const int code = plan.ops[op];
+        if (code < 0) {
+            const double rr = stack[--sp];
+            const double ll = stack[--sp];
+            stack[sp++] = ll + rr;
+            continue;
+        }
+        const int n = plan.leaf_len[code];
+        double res = 0.0;
+        if (n < 8) {
+            for (int i = 0; i < n; ++i) {
+                const double v = normal();
+                store(j++, v);
+                res += v * v;
+            }
+        } else {
+            double r[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            const int n8 = n - (n % 8);
+            for (int i0 = 0; i0 < n8; i0 += 8) {
+#if defined(__HIPCC__)
+#pragma unroll
+#endif
+                for (int k = 0; k < 8; ++k) {
+                    const double v = normal();
+                    store(j++, v);
+                    r[k] += v * v;
+                }
+            }
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (int i = n8; i < n; ++i) {
+                const double v = normal();
+                store(j++, v);
+                res += v * v;
+            }
+        }
+        if (plan.nops == 1) return res;
+        stack[sp++] = res;
+    }
+    return d > 0 ? stack[0] : 0.0;
 }

@@ -31,20 +31,10 @@ void h_gT(uint64_t seed, int64_t T, int64_t run, int64_t d, double* z, double* y
     Ki ki; Wi wi; Fi fi;
     ocx_pw_plan plan; ocx_pw_build(&plan, (int)d);
     for (int64_t t = 0; t < T; ++t) {
-        double stack[16]; int sp = 0;
-        double* row = z + t * d; int64_t j = 0;
-        for (int op = 0; op < plan.nops; ++op) {
-            int code = plan.ops[op];
-            if (code >= 0) {
-                ocx_pw_leaf leaf; ocx_pw_leaf_begin(&leaf, plan.leaf_len[code]);
-                for (int i = 0; i < plan.leaf_len[code]; ++i, ++j) {
-                    row[j] = ocx_standard_normal(&g, ki, wi, fi);
-                    ocx_pw_leaf_add(&leaf, row[j] * row[j]);
-                }
-                stack[sp++] = leaf.res;
-            } else { double r = stack[--sp]; double l = stack[--sp]; stack[sp++] = l + r; }
-        }
-        double nrm = sqrt(d > 0 ? stack[0] : 0.0);
+        double* row = z + t * d;
+        double sumsq = ocx_row_sumsq((int)d, plan, [&]() { return ocx_standard_normal(&g, ki, wi, fi); },
+                                     [&](int j, double v) { row[j] = v; });
+        double nrm = sqrt(sumsq);
         double sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);
         for (int64_t k = 0; k < d; ++k) row[k] *= sc;
     }
