@@ -149,6 +149,97 @@ OCX_HD void ocx_rng_init3(ocx_pcg64* g, uint64_t w0, uint64_t w1, uint64_t w2) {
 }
 
 // ---------------------------------------------------------------------------
+// log1p exactly as the host libm computes it (glibc 2.35, dbl-64/s_log1p.c: the
+// fdlibm algorithm with glibc's Estrin-form polynomial).  NumPy's ziggurat tail
+// (npy_log1p → libm log1p) turns its result straight into a normal deviate, so the
+// device must reproduce libm bit for bit, not merely to 1 ulp; tests/test_rng_host.py
+// checks this restatement against math.log1p on millions of inputs.
+// Algorithm and constants: fdlibm, Copyright (C) 1993 by Sun Microsystems, Inc.
+// Permission to use, copy, modify, and distribute this software is freely granted,
+// provided that this notice is preserved.
+// ---------------------------------------------------------------------------
+OCX_HD int32_t ocx_hiword(double x) {
+    return (int32_t)(__builtin_bit_cast(uint64_t, x) >> 32);
+}
+OCX_HD double ocx_with_hiword(double x, int32_t h) {
+    const uint64_t lo = __builtin_bit_cast(uint64_t, x) & 0xffffffffULL;
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)h << 32) | lo);
+}
+
+OCX_HD double ocx_log1p(double x) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+                 two54 = 1.80143985094819840000e+16;
+    const double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
+                 Lp3 = 2.857142874366239149e-01, Lp4 = 2.222219843214978396e-01,
+                 Lp5 = 1.818357216161805012e-01, Lp6 = 1.531383769920937332e-01,
+                 Lp7 = 1.479819860511658591e-01;
+    double hfsq, f = 0.0, c = 0.0, s, z, R, u;
+    int32_t k, hu = 0;
+    const int32_t hx = ocx_hiword(x);
+    const int32_t ax = hx & 0x7fffffff;
+    k = 1;
+    if (hx < 0x3FDA827A) {                     /* x < 0.41422 */
+        if (ax >= 0x3ff00000) {                /* x <= -1.0 */
+            if (x == -1.0) return -two54 / 0.0;
+            return (x - x) / (x - x);
+        }
+        if (ax < 0x3e200000) {                 /* |x| < 2**-29 */
+            if (ax < 0x3c900000) return x;     /* |x| < 2**-54 */
+            return x - x * x * 0.5;
+        }
+        if (hx > 0 || hx <= (int32_t)0xbfd2bec3) { /* -0.2929 < x < 0.41422 */
+            k = 0;
+            f = x;
+            hu = 1;
+        }
+    }
+    if (hx >= 0x7ff00000) return x + x;
+    if (k != 0) {
+        if (hx < 0x43400000) {
+            u = 1.0 + x;
+            hu = ocx_hiword(u);
+            k = (hu >> 20) - 1023;
+            c = (k > 0) ? 1.0 - (u - x) : x - (u - 1.0); /* correction term */
+            c /= u;
+        } else {
+            u = x;
+            hu = ocx_hiword(u);
+            k = (hu >> 20) - 1023;
+            c = 0.0;
+        }
+        hu &= 0x000fffff;
+        if (hu < 0x6a09e) {
+            u = ocx_with_hiword(u, hu | 0x3ff00000); /* normalize u */
+        } else {
+            k += 1;
+            u = ocx_with_hiword(u, hu | 0x3fe00000); /* normalize u/2 */
+            hu = (0x00100000 - hu) >> 2;
+        }
+        f = u - 1.0;
+    }
+    hfsq = 0.5 * f * f;
+    if (hu == 0) { /* |f| < 2**-20 */
+        if (f == 0.0) {
+            if (k == 0) return 0.0;
+            c += k * ln2_lo;
+            return k * ln2_hi + c;
+        }
+        R = hfsq * (1.0 - 0.66666666666666666 * f);
+        if (k == 0) return f - R;
+        return k * ln2_hi - ((R - (k * ln2_lo + c)) - f);
+    }
+    s = f / (2.0 + f);
+    z = s * s;
+    const double R1 = z * Lp1, z2 = z * z;
+    const double R2 = Lp2 + z * Lp3, z4 = z2 * z2;
+    const double R3 = Lp4 + z * Lp5, z6 = z4 * z2;
+    const double R4 = Lp6 + z * Lp7;
+    R = R1 + z2 * R2 + z4 * R3 + z6 * R4;
+    if (k == 0) return f - (hfsq - s * (hfsq + R));
+    return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
+}
+
+// ---------------------------------------------------------------------------
 // Ziggurat standard normal (NumPy random_standard_normal).  The three tables are
 // passed in so the device kernel can serve them from LDS.
 // ---------------------------------------------------------------------------
@@ -164,8 +255,8 @@ OCX_HD double ocx_standard_normal_slow(ocx_pcg64* g, const KiT& ki, const WiT& w
     for (;;) {
         if (idx == 0) {
             for (;;) {
-                double xx = -OCX_ZIG_NOR_INV_R * log1p(-ocx_pcg_next_double(g));
-                double yy = -log1p(-ocx_pcg_next_double(g));
+                double xx = -OCX_ZIG_NOR_INV_R * ocx_log1p(-ocx_pcg_next_double(g));
+                double yy = -ocx_log1p(-ocx_pcg_next_double(g));
                 if (yy + yy > xx * xx)
                     return ((rabs >> 8) & 0x1) ? -(OCX_ZIG_NOR_R + xx) : OCX_ZIG_NOR_R + xx;
             }

@@ -12,6 +12,8 @@ struct Wi { double operator()(int i) const { return bits2d(OCX_ZIG_WI_BITS[i]); 
 struct Fi { double operator()(int i) const { return bits2d(OCX_ZIG_FI_BITS[i]); } };
 
 extern "C" {
+void h_log1p(const double* x, int64_t n, double* out) { for (int64_t i = 0; i < n; ++i) out[i] = ocx_log1p(x[i]); }
+
 void h_seedseq_state4(const uint32_t* words, int n, uint64_t* out) { ocx_seedseq_state4(words, n, out); }
 
 void h_raw(uint64_t w0, uint64_t w1, uint64_t w2, int64_t n, uint64_t* out) {

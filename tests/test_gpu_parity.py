@@ -136,7 +136,7 @@ def test_published_gT_curve(ocx):
 # ------------------------------------------------------------------ generator
 @pytest.mark.parametrize("B,T,d,P", [(70, 50, 5, 1), (33, 20, 64, 4), (5, 8, 1024, 64),
                                      (40, 9, 129, 0), (3, 11, 2, 0), (9, 6, 64, -1),
-                                     (17, 7, 100, -2)])
+                                     (17, 7, 100, -2), (192, 2000, 64, 1)])
 def test_device_generator_matches_numpy(ocx, B, T, d, P):
     import torch
     eng = ocx["engine"]
@@ -144,9 +144,10 @@ def test_device_generator_matches_numpy(ocx, B, T, d, P):
     torch.cuda.synchronize()
     z = untile_z(db.z.cpu().numpy(), db.L)
     y = untile_y(db.y.cpu().numpy(), db.L)
+    # (192, 2000, 64): ~6700 ziggurat tail draws → the device log1p must equal libm's
     for b in range(B):
         zr, yr = O.gT_sample(0, T, 10 + b, d)
-        assert np.array_equal(z[b], zr), b
+        assert np.array_equal(z[b], zr), (b, int((z[b] != zr).sum()))
         assert np.array_equal(y[b], yr), b
     # padding (coordinates >= d, sequences >= B) is zero
     zt = db.z.cpu().numpy()

@@ -32,6 +32,7 @@ def lib():
     L.h_raw.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_int64, u64p]
     L.h_normals.argtypes = [ctypes.c_uint64] * 3 + [ctypes.c_int64, dp]
     L.h_gT.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, dp, dp]
+    L.h_log1p.argtypes = [dp, ctypes.c_int64, dp]
     return L
 
 
@@ -85,3 +86,17 @@ def test_gT_sampler(lib, T, d, run):
     yr = gen.choice([-1.0, 1.0], size=T)
     assert np.array_equal(z, zr)
     assert np.array_equal(y, yr)
+
+
+def test_log1p_matches_libm(lib):
+    """The ziggurat tail uses log1p(-u), u in [0, 1): the restatement must equal the host
+    libm (what NumPy calls) bit for bit, not just to 1 ulp."""
+    import math
+    rng = np.random.default_rng(3)
+    x = np.concatenate([-rng.random(400000), -rng.random(50000) * 1e-3,
+                        -np.ldexp(rng.random(50000), -rng.integers(20, 60, 50000)),
+                        rng.random(50000) * 3.0, [0.0, -0.0, -0.5, -1e-300, 1e300, -1.0]])
+    out = np.zeros_like(x)
+    lib.h_log1p(_dp(x), len(x), _dp(out))
+    ref = np.array([math.log1p(v) if v > -1.0 else (-math.inf) for v in x])
+    assert np.array_equal(out, ref)
