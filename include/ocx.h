@@ -23,8 +23,9 @@
  *       0      auto: the fewest lanes that fill the GPU; partial sums combined by a
  *              butterfly (~1e-16 relative to the reference's sequential sums);
  *       k >= 2 k lanes (power of two), butterfly sums;
- *       1      exact, auto lanes (<= 4 unless d needs more): every sum in the
- *              reference's sequential order, so results are bit-identical;
+ *       1      exact, auto lanes (<= 16 coordinates per lane, <= 4 lanes unless d
+ *              needs more): every sum in the reference's sequential order, so
+ *              results are bit-identical;
  *       -k     exact with k lanes; for k > 1 the running sum is handed from lane to
  *              lane (layout.chain = 1).
  */
@@ -113,6 +114,19 @@ int ocx_dev_pack(const ocx_layout* L, const double* z, const double* y, double* 
  * _rng(base_seed, T, run0 + b) → clipped N(0, I_d) rows and ±1 labels. */
 int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* z_tiled,
                    double* y_tiled, void* stream);
+
+/* sequence_generation.py families on device, sequence b of the layout:
+ *   family 1  make_random_iid_stream (:54-69): _rng(run_seeds[b], T, stream_ids[b]),
+ *             u from _rng(run_seeds[b], 0, 11); fp32 rows, y = sign(z.u) (0 → +1);
+ *   family 2  make_noisy_iid_stream (:72-89): u from stream 21, labels flipped where
+ *             gen.random(T) < p;
+ *   family 3  flip_sequence (:24-28);  family 4  switching_two_leaders_sequence
+ *             (:36-47) with block_len.  Families 3/4 ignore the seed arrays.
+ * run_seeds / stream_ids are device uint64 [B].  The float32 rows are stored as the
+ * float64 values simulate_alg's np.ascontiguousarray(z, float64) would see. */
+int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
+                       const uint64_t* stream_ids, double p, int64_t block_len, double* z_tiled,
+                       double* y_tiled, void* stream);
 
 /* fast_algorithms.py:88-115 on device.  comparator [B][d] device, nullable.
  * Outputs are device arrays [B] (nullable) and x_last [B][d] (nullable). */

@@ -53,6 +53,8 @@ SIGNATURES = {
     "ocx_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp, c_int, c_int]),
     "ocx_dev_pack": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_dev_gen_gT": (c_int, [ctypes.POINTER(Layout), c_u64, c_i64, c_vp, c_vp, c_vp]),
+    "ocx_dev_gen_family": (c_int, [ctypes.POINTER(Layout), c_int, c_vp, c_vp, c_double, c_i64,
+                                   c_vp, c_vp, c_vp]),
     "ocx_dev_simulate_alg": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp,
                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_dev_simulate_smart": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_double, c_vp,

@@ -127,13 +127,19 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     while (p_min < 64 && ceil_div(d, p_min) > 64) p_min *= 2;
     int64_t p_max = 1;
     while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
-    if (lanes_per_seq == 0 || lanes_per_seq == 1) {
+    if (lanes_per_seq == 0) {
         // auto: enough lanes for ~8 wavefronts per CU (131072 lanes on
-        // 256 CUs) when B allows; exact mode caps the chain at 4 lanes.
+        // 256 CUs) when B allows.
         int64_t p_lanes = 1;
         while (p_lanes < 64 && p_lanes * B < 131072) p_lanes *= 2;
-        int64_t hi = exact ? std::min<int64_t>(p_max, 4) : p_max;
-        P = (int)std::max(p_min, std::min(p_lanes, std::max<int64_t>(hi, 1)));
+        P = (int)std::max(p_min, std::min(p_lanes, p_max));
+    } else if (lanes_per_seq == 1) {
+        // exact auto: at most 16 coordinates per lane (register budget of the chained
+        // sums), then up to 4 lanes while that is needed to reach 65536 lanes.
+        int64_t p = 1;
+        while (p < 64 && ceil_div(d, p) > 16) p *= 2;
+        while (p < 4 && p * B < 65536 && ceil_div(d, 2 * p) >= 2) p *= 2;
+        P = (int)p;
     }
     if (P < 1 || P > 64 || (P & (P - 1)) != 0)
         return fail(OCX_E_INVALID, "lanes_per_seq must be 0, 1, or +/- a power of two <= 64");
@@ -190,6 +196,22 @@ int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double
     if (run0 < 0) return fail(OCX_E_INVALID, "run0 < 0");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
     OCX_HIP(ocx_launch_gen_gT(L, base_seed, run0, z_tiled, y_tiled, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
+                       const uint64_t* stream_ids, double p, int64_t block_len, double* z_tiled,
+                       double* y_tiled, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (family < 1 || family > 4) return fail(OCX_E_INVALID, "family must be 1..4");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
+    if ((family == 1 || family == 2) && L->B > 0 && (!run_seeds || !stream_ids))
+        return fail(OCX_E_INVALID, "NULL seed arrays");
+    if ((family == 1 || family == 2) && (int64_t)L->P * L->C > 64)
+        return fail(OCX_E_UNSUPPORTED, "random families need a padded row <= 64 coordinates");
+    if (family == 4 && block_len < 1) return fail(OCX_E_INVALID, "block_len < 1");
+    OCX_HIP(ocx_launch_gen_family(L, family, run_seeds, stream_ids, p, block_len, z_tiled,
+                                  y_tiled, (hipStream_t)stream));
     return OCX_OK;
 }
 

@@ -19,3 +19,6 @@ hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st);
+hipError_t ocx_launch_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
+                                 const uint64_t* stream_ids, double p, int64_t block_len,
+                                 double* zt, double* ytl, hipStream_t st);

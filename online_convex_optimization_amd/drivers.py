@@ -1,0 +1,107 @@
+"""Batched, device-resident versions of the reference's experiment sweeps.
+
+``evaluate_stream_with_stats`` (fast_driver.py:71-127) calls simulate_alg / SMART
+once per (run, T, replicate) on host-built sequences.  Here every (run, replicate)
+sequence of one T is generated on the GPU in a single batch (its ``sequence_generation``
+family, bit-identical to the NumPy streams), the four algorithms run as four kernel
+launches over that batch, and only the 4·runs·replicates regrets come back.  The
+averaging then uses the same NumPy calls as the reference (fast_driver.py:113-125), so
+the statistics are identical, not merely close.
+
+``fast_driver_main`` is fast_driver.py:201-220 without the plotting: the g(T) sweep
+(empirical_worst_case_thresholds) followed by the four cases.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import engine
+from .fast_algorithms import empirical_worst_case_thresholds
+from .sequence_generation import REPLICATES_BY_TITLE, RUNS_BY_TITLE
+
+ALGO_KEYS = ("FTRL", "FTL", "SMART", "EMP")
+CI_Z = 1.96
+SQRT2 = math.sqrt(2)
+
+# CASES title → (device family, stream-id base of the replicate streams, d)
+CASE_FAMILIES = {
+    "Random i.i.d. (separable)": ("iid", 13),
+    "Massart noise 10%": ("massart", 23),
+    "Label flips": ("flip", 0),
+    "Switching leaders": ("switching", 0),
+}
+
+Stats = Dict[str, Tuple[np.ndarray, np.ndarray]]
+
+
+def _sem(x: np.ndarray) -> float:
+    """fast_driver.py:59-63."""
+    n = x.size
+    if n <= 1:
+        return 0.0
+    return float(np.std(x, ddof=1) / math.sqrt(n))
+
+
+def case_regrets(title: str, T: int, g_emp_T: float, *, runs: int, replicates: int,
+                 base_seed: int = 0, d: int = 5, p: float = 0.10, block_len: int = 20,
+                 lanes_per_seq: int = 1, device: int = 0) -> Dict[str, np.ndarray]:
+    """Regrets [runs, replicates] of FTRL, FTL, SMART(sqrt 2T), SMART(g_emp) for one case
+    and one T — fast_driver.py:86-111 for every (run, rep) at once, on device."""
+    family, stream0 = CASE_FAMILIES[title]
+    B = runs * replicates
+    db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes_per_seq, device=device)
+    run_idx = np.repeat(np.arange(runs), replicates)
+    rep_idx = np.tile(np.arange(replicates), runs)
+    run_seeds = base_seed + 2025 * (run_idx + 1)  # fast_driver.py:88
+    db.generate_family(family, run_seeds, stream0 + rep_idx, p=p, block_len=block_len)
+    out = {}
+    out["FTRL"] = db.simulate_alg(0, SQRT2).clone()
+    out["FTL"] = db.simulate_alg(1, SQRT2).clone()
+    out["SMART"] = db.simulate_smart(math.sqrt(2 * T), SQRT2).clone()
+    out["EMP"] = db.simulate_smart(float(g_emp_T), SQRT2).clone()
+    return {k: v[:B].cpu().numpy().reshape(runs, replicates) for k, v in out.items()}
+
+
+def evaluate_stream_with_stats(title: str, T_grid: Sequence[int], g_emp: Mapping[int, float], *,
+                               runs: int = 1, replicates: int = 1, base_seed: int = 0,
+                               lanes_per_seq: int = 1, device: int = 0) -> Stats:
+    """fast_driver.py:71-127 for the CASES entry ``title``: mean regret and 95 % CI per T."""
+    by_T = {k: [[] for _ in range(len(T_grid))] for k in ALGO_KEYS}
+    per_T = [case_regrets(title, int(T), g_emp[int(T)], runs=runs, replicates=replicates,
+                          base_seed=base_seed, lanes_per_seq=lanes_per_seq, device=device)
+             for T in T_grid]
+    for run in range(runs):
+        for ti in range(len(T_grid)):
+            for k in ALGO_KEYS:
+                by_T[k][ti].append(float(np.mean(list(per_T[ti][k][run]))))
+    stats: Stats = {}
+    for k in ALGO_KEYS:
+        means, cis = [], []
+        for vals in by_T[k]:
+            arr = np.asarray(vals, dtype=float)
+            mu = float(np.mean(arr)) if arr.size else 0.0
+            ci = CI_Z * _sem(arr) if arr.size > 1 else 0.0
+            means.append(mu)
+            cis.append(ci)
+        stats[k] = (np.array(means, dtype=float), np.array(cis, dtype=float))
+    return stats
+
+
+def fast_driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 1000,
+                     base_seed: int = 0, runs_by_title: Optional[Mapping[str, int]] = None,
+                     replicates_by_title: Optional[Mapping[str, int]] = None,
+                     device: int = 0) -> Tuple[Dict[int, float], Dict[str, Stats]]:
+    """fast_driver.py:201-220 minus the figures: (g_emp, stats_by_case)."""
+    T_grid = list(range(100, 1100, 100)) if T_grid is None else [int(t) for t in T_grid]
+    runs_by_title = RUNS_BY_TITLE if runs_by_title is None else runs_by_title
+    replicates_by_title = REPLICATES_BY_TITLE if replicates_by_title is None else replicates_by_title
+    g_emp = empirical_worst_case_thresholds(np.asarray(T_grid), runs=g_runs, base_seed=base_seed)
+    stats = {}
+    for title in CASE_FAMILIES:
+        stats[title] = evaluate_stream_with_stats(
+            title, T_grid, g_emp, runs=runs_by_title.get(title, 1),
+            replicates=replicates_by_title.get(title, 1), base_seed=base_seed, device=device)
+    return g_emp, stats

@@ -179,6 +179,29 @@ class DeviceBatch:
                   self.y.data_ptr(), self._sp)
         return self
 
+    FAMILIES = {"iid": 1, "massart": 2, "flip": 3, "switching": 4}
+
+    def generate_family(self, family, run_seeds=None, stream_ids=None, *, p: float = 0.10,
+                        block_len: int = 20):
+        """Fill z/y with a sequence_generation.py family (ocx_dev_gen_family): for the
+        random families sequence b is _rng(run_seeds[b], T, stream_ids[b])."""
+        torch = self.torch
+        fam = self.FAMILIES[family] if isinstance(family, str) else int(family)
+        rs = si = None
+        if fam in (1, 2):
+            rs = torch.as_tensor(np.asarray(run_seeds, dtype=np.uint64).astype(np.int64)
+                                 ).to(self.device)
+            si = torch.as_tensor(np.asarray(stream_ids, dtype=np.uint64).astype(np.int64)
+                                 ).to(self.device)
+            if rs.numel() != self.L.B or si.numel() != self.L.B:
+                raise ValueError("need one run seed and one stream id per sequence")
+        _lib.call("ocx_dev_gen_family", self._lp(), fam,
+                  rs.data_ptr() if rs is not None else None,
+                  si.data_ptr() if si is not None else None, float(p), int(block_len),
+                  self.z.data_ptr(), self.y.data_ptr(), self._sp)
+        self._keep_seeds = (rs, si)
+        return self
+
     def pack(self, z, y):
         """Copy host/device arrays z [B,T,d], y [B,T] into the tiled layout."""
         torch = self.torch

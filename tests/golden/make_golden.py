@@ -198,6 +198,21 @@ def main():
                     })
     out["streams"] = streams
 
+    # ---------------- fast_driver.evaluate_stream_with_stats (reduced sizes) ------------
+    import fast_driver as fd  # the reference driver (matplotlib/tqdm import only)
+    drv = {"T_grid": [100, 200], "g_emp": {"100": H(PUBLISHED_GT[0]), "200": H(PUBLISHED_GT[1])},
+           "cases": {}}
+    g_small = {100: PUBLISHED_GT[0], 200: PUBLISHED_GT[1]}
+    for title, builder in sg.CASES.items():
+        runs = 3 if title.startswith(("Random", "Massart")) else 1
+        reps = 2 if runs > 1 else 1
+        st = fd.evaluate_stream_with_stats(builder, np.array([100, 200]), g_small, runs=runs,
+                                           replicates=reps, base_seed=0, stream_name=title)
+        drv["cases"][title] = {"runs": runs, "replicates": reps,
+                               "stats": {k: [[H(v) for v in m], [H(v) for v in c]]
+                                         for k, (m, c) in st.items()}}
+    out["driver"] = drv
+
     # ---------------- published end-to-end KAT: g(T), runs=1000, d=5 --------------------
     if not args.skip_gT_kat:
         t0 = time.time()

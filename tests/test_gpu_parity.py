@@ -244,3 +244,60 @@ def test_full_size_properties(ocx):
         assert r1[b] == O.simulate_alg(zr, yr, 0, SQ2), b
     del exact, auto
     torch.cuda.empty_cache()
+
+
+# ------------------------------------------------------------------ sequence families
+@pytest.mark.parametrize("family,runs,reps,T", [("iid", 48, 16, 1000), ("massart", 48, 20, 300),
+                                                ("iid", 3, 2, 100), ("massart", 2, 3, 1000)])
+def test_device_families_match_numpy(ocx, family, runs, reps, T):
+    """Device-generated random families == the reference's builders (fp32 rows, labels
+    sign(z @ u) through this host's BLAS order, Massart flips) for every (run, rep)."""
+    import torch
+    eng = ocx["engine"]
+    base = 0
+    stream0 = 13 if family == "iid" else 23
+    run_idx = np.repeat(np.arange(runs), reps)
+    rep_idx = np.tile(np.arange(reps), runs)
+    seeds = base + 2025 * (run_idx + 1)
+    db = eng.DeviceBatch(runs * reps, T, 5, lanes_per_seq=1)
+    db.generate_family(family, seeds, stream0 + rep_idx)
+    torch.cuda.synchronize()
+    z = untile_z(db.z.cpu().numpy(), db.L)
+    y = untile_y(db.y.cpu().numpy(), db.L)
+    bad_y = 0
+    for b in range(runs * reps):
+        if family == "iid":
+            zr, yr, _ = O.random_iid_sample(int(seeds[b]), T, int(rep_idx[b]))
+        else:
+            zr, yr, _ = O.noisy_iid_sample(int(seeds[b]), T, int(rep_idx[b]))
+        assert np.array_equal(z[b], zr.astype(np.float64)), b
+        bad_y += int((y[b] != yr.astype(np.float64)).sum())
+    assert bad_y == 0
+
+
+def test_device_fixed_families(ocx):
+    import torch
+    eng = ocx["engine"]
+    for name, fn in (("flip", O.flip_sequence), ("switching", O.switching_two_leaders_sequence)):
+        for T, d, P in ((1000, 5, 1), (77, 64, 4), (40, 3, 0)):
+            db = eng.DeviceBatch(3, T, d, lanes_per_seq=P).generate_family(name)
+            torch.cuda.synchronize()
+            z = untile_z(db.z.cpu().numpy(), db.L)
+            y = untile_y(db.y.cpu().numpy(), db.L)
+            zr, yr, _ = fn(T, d=d)
+            for b in range(3):
+                assert np.array_equal(z[b], zr.astype(np.float64)), (name, T, d)
+                assert np.array_equal(y[b], yr.astype(np.float64)), (name, T, d)
+
+
+def test_driver_stats_golden(ocx, golden):
+    """fast_driver.evaluate_stream_with_stats on device == the reference driver's output."""
+    from online_convex_optimization_amd import drivers
+    drv = golden.j["driver"]
+    g_emp = {int(k): F(v) for k, v in drv["g_emp"].items()}
+    for title, rec in drv["cases"].items():
+        st = drivers.evaluate_stream_with_stats(title, drv["T_grid"], g_emp, runs=rec["runs"],
+                                                replicates=rec["replicates"])
+        for k, (m, c) in rec["stats"].items():
+            assert np.array_equal(st[k][0], np.array([F(v) for v in m])), (title, k)
+            assert np.array_equal(st[k][1], np.array([F(v) for v in c])), (title, k)
