@@ -47,6 +47,9 @@ def parse():
                          "reference, auto lanes), 0 = auto with butterfly sums, k / -k explicit")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU-baseline sample (0 disables)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (rehearsal: ranks may "
+                         "share a GPU, the regret gather goes through host memory)")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -78,10 +81,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = local % torch.cuda.device_count() if a.dist_backend == "gloo" else local
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    local = gpu
     stream = torch.cuda.current_stream(dev)
 
     B, T, d = a.B, a.T, a.d
@@ -91,12 +99,18 @@ def main():
     db.generate_gT(base_seed=0, run0=run0)
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - tg0
-    gathered = torch.zeros(world * B, dtype=torch.float64, device=dev) if world > 1 else None
+    gdev = dev if a.dist_backend == "nccl" else torch.device("cpu")
+    gathered = torch.zeros(world * B, dtype=torch.float64, device=gdev) if world > 1 else None
+
+    def gather():
+        # the path's one exchange: every rank's regrets to every rank
+        src = db.regret[:B] if gdev == dev else db.regret[:B].cpu()
+        dist.all_gather_into_tensor(gathered, src)
 
     def step():
         db.simulate_alg(0, math.sqrt(2))
         if world > 1:
-            dist.all_gather_into_tensor(gathered, db.regret[:B])
+            gather()
 
     for _ in range(a.warmup):
         step()
@@ -111,13 +125,13 @@ def main():
         db.simulate_alg(0, math.sqrt(2))
         ev[i][1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, db.regret[:B])
+            gather()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
@@ -178,7 +192,12 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "gen_seconds": gen_s,
+            "gen_timesteps_per_s": B * T / gen_s,
         }
+        if world > 1:
+            g = gathered.cpu().numpy()
+            out["gathered_check"] = bool(np.array_equal(g[:B], regrets))
+            out["dist_backend"] = a.dist_backend
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -22,8 +22,9 @@ BUILD = os.path.join(ROOT, "build", "ocx")
 LIB = os.path.join(PKG, "libocx.so")
 ARCH = os.environ.get("OCX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["ocx_sim.hip", "ocx_gen.hip", "ocx_capi.hip"]
-HEADERS = ["ocx_internal.h", "ocx_rng.h", "ocx_sim_kernels.h", "zig_tables.h"]
+SOURCES = ["ocx_sim.hip", "ocx_gen.hip", "ocx_stream.hip", "ocx_capi.hip"]
+HEADERS = ["ocx_internal.h", "ocx_rng.h", "ocx_sim_kernels.h", "zig_tables.h",
+           "ocx_device_math.h", "ocx_dispatch.h"]
 
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -58,6 +59,7 @@ struct DevCtx {
     bool init = false;
     hipStream_t stream = nullptr;
     DevBuf zraw, yraw, zt, yt, at, araw, cmp, thr, out, sw;
+    DevBuf rstate, lstate, theta, acc;  // long-horizon (T-chunked) g(T) sweep
 };
 
 DevCtx g_ctx[kMaxDevices];
@@ -376,29 +378,83 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
 
 int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
                    double eta0, double* regrets, int lanes_per_seq, int device) {
-    if (R < 0 || run0 < 0) return fail(OCX_E_INVALID, "negative run range");
+    if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
     if (R == 0) return OCX_OK;
     if (!regrets) return fail(OCX_E_INVALID, "NULL regrets");
     DevCtx* cx;
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);
     hipStream_t st = cx->stream;
-    // chunk the runs so the tiled z of one chunk stays <= ~16 GiB
-    const int64_t per_seq = std::max<int64_t>(T * (d + 1) * 8, 8);
-    int64_t chunk = std::max<int64_t>((int64_t)16 << 30, 0) / per_seq;
-    chunk = std::max<int64_t>(64, std::min<int64_t>(chunk, R));
-    OCX_HIP(cx->out.ensure((size_t)std::min(chunk, R) * 8));
-    for (int64_t r0 = 0; r0 < R; r0 += chunk) {
-        const int64_t nb = std::min(chunk, R - r0);
-        ocx_layout L;
-        if (int rc = ocx_layout_init(nb, T, d, lanes_per_seq, &L)) return rc;
-        OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
-        OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
-        OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(), cx->yt.as<double>(),
-                                  st));
-        OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
-                               cx->out.as<double>(), nullptr, nullptr, nullptr, st));
-        OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
+    // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB, default 64 GiB)
+    int64_t budget = (int64_t)64 << 30;
+    if (const char* e = std::getenv("OCX_HBM_BUDGET_GB")) budget = (int64_t)(std::atof(e) * (1 << 30));
+    const int64_t kBatch = 131072;  // concurrent streams that fill the generator
+    ocx_layout L1;
+    if (int rc = ocx_layout_init(std::min<int64_t>(R, kBatch), std::max<int64_t>(T, 1), d,
+                                 lanes_per_seq, &L1))
+        return rc;
+    const int64_t step_bytes = (L1.z_elems + L1.y_elems) * 8 / std::max<int64_t>(T, 1);
+    const bool streamed = step_bytes * T > budget && L1.Dp <= 64;
+    if (!streamed) {
+        // whole horizon resident: as many runs per batch as the budget holds
+        const int64_t per_seq = std::max<int64_t>(step_bytes * T / std::max<int64_t>(L1.B, 1), 8);
+        int64_t chunk = std::max<int64_t>(64, std::min<int64_t>(budget / per_seq, R));
+        OCX_HIP(cx->out.ensure((size_t)chunk * 8));
+        for (int64_t r0 = 0; r0 < R; r0 += chunk) {
+            const int64_t nb = std::min(chunk, R - r0);
+            ocx_layout L;
+            if (int rc = ocx_layout_init(nb, T, d, lanes_per_seq, &L)) return rc;
+            OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+            OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+            OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
+                                      cx->yt.as<double>(), st));
+            OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
+                                   cx->out.as<double>(), nullptr, nullptr, nullptr, st));
+            OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8,
+                                   hipMemcpyDeviceToHost, st));
+            OCX_HIP(hipStreamSynchronize(st));
+        }
+        return OCX_OK;
+    }
+    // streamed: batches of kBatch runs, horizon cut into chunks of Tc steps
+    // (ocx_stream.hip): seek → pass A (generate chunk, advance theta) → pass B
+    // (regenerate chunk, comparator loss) with the PCG states saved at chunk starts.
+    const int64_t Tc = std::max<int64_t>(1, budget / std::max<int64_t>(step_bytes, 1));
+    const int64_t nch = (T + Tc - 1) / Tc;
+    const int64_t Bc = L1.B;
+    OCX_HIP(cx->rstate.ensure((size_t)(nch + 1) * Bc * 48));
+    OCX_HIP(cx->lstate.ensure((size_t)(nch + 1) * Bc * 48));
+    OCX_HIP(cx->theta.ensure((size_t)Bc * L1.Dp * 8));
+    OCX_HIP(cx->acc.ensure((size_t)Bc * 3 * 8));
+    for (int64_t r0 = 0; r0 < R; r0 += Bc) {
+        const int64_t nb = std::min(Bc, R - r0);
+        uint64_t* rs = cx->rstate.as<uint64_t>();
+        uint64_t* ls = cx->lstate.as<uint64_t>();
+        double* th = cx->theta.as<double>();
+        double* cum = cx->acc.as<double>();
+        double* comp = cum + Bc;
+        double* reg = comp + Bc;
+        OCX_HIP(ocx_launch_gen_seek(base_seed, T, run0 + r0, nb, d, rs, ls, st));
+        OCX_HIP(hipMemsetAsync(th, 0, (size_t)nb * L1.Dp * 8, st));
+        OCX_HIP(hipMemsetAsync(cum, 0, (size_t)Bc * 2 * 8, st));
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int64_t c = 0; c < nch; ++c) {
+                const int64_t t0 = c * Tc, tl = std::min(Tc, T - t0);
+                ocx_layout L;
+                if (int rc = ocx_layout_init(nb, tl, d, lanes_per_seq, &L)) return rc;
+                OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+                OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+                uint64_t* rin = rs + (size_t)c * Bc * 6;
+                uint64_t* lin = ls + (size_t)c * Bc * 6;
+                OCX_HIP(ocx_launch_gen_gT_chunk(&L, T, rin, pass == 0 ? rin + Bc * 6 : nullptr, lin,
+                                                pass == 0 ? lin + Bc * 6 : nullptr,
+                                                cx->zt.as<double>(), cx->yt.as<double>(), st));
+                OCX_HIP(ocx_launch_alg_chunk(&L, cx->zt.as<double>(), cx->yt.as<double>(), t0, 0,
+                                             eta0, pass, th, cum, comp,
+                                             (pass == 1 && c == nch - 1) ? reg : nullptr, st));
+            }
+        }
+        OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
         OCX_HIP(hipStreamSynchronize(st));
     }
     return OCX_OK;

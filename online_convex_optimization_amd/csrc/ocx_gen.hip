@@ -34,6 +34,24 @@ __device__ __forceinline__ void load_tables(Tables& tb) {
     }
 }
 
+// Saved PCG64 stream state in HBM: 6 x u64 per sequence
+// [state lo, state hi, inc lo, inc hi, buf32 | has32 << 32, 0].
+__device__ __forceinline__ void load_state(ocx_pcg64* g, const uint64_t* p) {
+    g->state = ((ocx_u128)p[1] << 64) | p[0];
+    g->inc = ((ocx_u128)p[3] << 64) | p[2];
+    g->buf32 = (uint32_t)p[4];
+    g->has32 = (int)(p[4] >> 32);
+}
+
+__device__ __forceinline__ void save_state(const ocx_pcg64* g, uint64_t* p) {
+    p[0] = (uint64_t)g->state;
+    p[1] = (uint64_t)(g->state >> 64);
+    p[2] = (uint64_t)g->inc;
+    p[3] = (uint64_t)(g->inc >> 64);
+    p[4] = (uint64_t)g->buf32 | ((uint64_t)(uint32_t)g->has32 << 32);
+    p[5] = 0;
+}
+
 }  // namespace
 
 // Per-family row recipes (template FAM of the staged kernel):
@@ -95,7 +113,12 @@ template <int FAM>
 __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
     uint64_t base_seed, int64_t T, int64_t run0, int64_t B, int d, int P, int C, int64_t G,
     const uint64_t* __restrict__ run_seeds, const uint64_t* __restrict__ stream_ids, double p,
-    double* __restrict__ zt, double* __restrict__ ytl) {
+    double* __restrict__ zt, double* __restrict__ ytl, int64_t T_seed,
+    const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
+    const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out) {
+    // GT chunk mode (st_in != nullptr): rows resume from st_in[b], T is the chunk length
+    // and T_seed the horizon the streams were seeded with; labels come from a second
+    // saved cursor lab_in[b] (the stream position after all T_seed·d normals).
     __shared__ Tables tb;
     __shared__ __attribute__((aligned(16))) double rows[64 * OCX_GEN_ROW];
     __shared__ float us[FAM == OCX_FAM_GT ? 1 : 64 * 65];
@@ -115,7 +138,8 @@ __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
     ocx_pcg64 rng;
     float* u = us + (FAM == OCX_FAM_GT ? 0 : lane * 65);
     if constexpr (FAM == OCX_FAM_GT) {
-        ocx_rng_init3(&rng, base_seed, (uint64_t)T, (uint64_t)(run0 + (live ? b : 0)));
+        if (st_in != nullptr && live) load_state(&rng, st_in + 6 * b);
+        else ocx_rng_init3(&rng, base_seed, (uint64_t)T_seed, (uint64_t)(run0 + (live ? b : 0)));
     } else {
         const uint64_t rs = live ? run_seeds[b] : 0;
         // u: _rng(run_seed, 0, 11 | 21).standard_normal(d) as fp32, / ||u|| (sdot)
@@ -174,14 +198,17 @@ __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
         }
         __syncthreads();
     }
+    if (FAM == OCX_FAM_GT && st_out != nullptr && live) save_state(&rng, st_out + 6 * b);
     if (gb >= G) return;
     if constexpr (FAM == OCX_FAM_GT) {
         // labels: choice([-1.0, 1.0], size=T) → integers(0, 2) → top bit of next_uint32
+        if (lab_in != nullptr && live) load_state(&rng, lab_in + 6 * b);
         for (int64_t t = 0; t < T; ++t) {
             double yv = 0.0;
             if (live) yv = (ocx_pcg_next32(&rng) >> 31) ? 1.0 : -1.0;
             yrow[t * S] = yv;
         }
+        if (lab_out != nullptr && live) save_state(&rng, lab_out + 6 * b);
     } else if constexpr (FAM == OCX_FAM_MASSART) {
         // flips = gen.random(T) < p; y[flips] *= -1.0
         if (live)
@@ -215,6 +242,37 @@ __global__ void ocx_gen_fixed_kernel(int family, int64_t block_len, int64_t B, i
         else yv = ((t / block_len) % 2 == 0) ? 1.0 : -1.0;              // blocks of +1, -1
         ytl[o] = (b < B) ? yv : 0.0;
     }
+}
+
+// Stream positions for chunked generation: st_out[b] = the fresh stream
+// _rng(base_seed, T_seed, run0 + b); lab_out[b] = the same stream after the T_seed·d
+// standard normals, i.e. where choice(T) starts drawing labels (fast_algorithms.py:234,239).
+// The ziggurat consumes a data-dependent number of raw draws, so the only way there is
+// to run it.
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_gen_seek_kernel(
+    uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t d,
+    uint64_t* __restrict__ st_out, uint64_t* __restrict__ lab_out) {
+    __shared__ Tables tb;
+    load_tables(tb);
+    __syncthreads();
+    auto ki = [&](int i) { return tb.ki[i]; };
+    auto wi = [&](int i) { return tb.wi[i]; };
+    auto fi = [&](int i) { return tb.fi[i]; };
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    ocx_pcg64 rng;
+    ocx_rng_init3(&rng, base_seed, (uint64_t)T_seed, (uint64_t)(run0 + b));
+    save_state(&rng, st_out + 6 * b);
+    double sink = 0.0;
+    const int64_t n = T_seed * d;
+    int64_t i = 0;
+    for (; i + 4 <= n; i += 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sink += ocx_standard_normal(&rng, ki, wi, fi);
+    }
+    for (; i < n; ++i) sink += ocx_standard_normal(&rng, ki, wi, fi);
+    save_state(&rng, lab_out + 6 * b);
+    if (sink == 1.2345e300) st_out[6 * b + 5] = 1;  // keep the draws alive (never true)
 }
 
 // General rows (padded width > 64): one lane per sequence, regenerate-to-scale.
@@ -277,7 +335,7 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
         const unsigned grid = (unsigned)((nlanes + 63) / 64);
         hipLaunchKernelGGL(ocx_gen_staged_kernel<OCX_FAM_GT>, dim3(grid), dim3(64), 0, st,
                            base_seed, L->T, run0, L->B, (int)L->d, L->P, L->C, L->G, nullptr,
-                           nullptr, 0.0, zt, ytl);
+                           nullptr, 0.0, zt, ytl, L->T, nullptr, nullptr, nullptr, nullptr);
     } else {
         const unsigned grid = (unsigned)((nlanes + OCX_BLOCK - 1) / OCX_BLOCK);
         hipLaunchKernelGGL(ocx_gen_regen_kernel, dim3(grid), dim3(OCX_BLOCK), 0, st, base_seed,
@@ -303,12 +361,35 @@ hipError_t ocx_launch_gen_family(const ocx_layout* L, int family, const uint64_t
     if (family == 1)
         hipLaunchKernelGGL(ocx_gen_staged_kernel<OCX_FAM_IID>, dim3(grid), dim3(64), 0, st,
                            (uint64_t)0, L->T, (int64_t)0, L->B, (int)L->d, L->P, L->C, L->G,
-                           run_seeds, stream_ids, p, zt, ytl);
+                           run_seeds, stream_ids, p, zt, ytl, L->T, nullptr, nullptr, nullptr,
+                           nullptr);
     else if (family == 2)
         hipLaunchKernelGGL(ocx_gen_staged_kernel<OCX_FAM_MASSART>, dim3(grid), dim3(64), 0, st,
                            (uint64_t)0, L->T, (int64_t)0, L->B, (int)L->d, L->P, L->C, L->G,
-                           run_seeds, stream_ids, p, zt, ytl);
+                           run_seeds, stream_ids, p, zt, ytl, L->T, nullptr, nullptr, nullptr,
+                           nullptr);
     else
         return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t ocx_launch_gen_seek(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
+                               int64_t d, uint64_t* st_out, uint64_t* lab_out, hipStream_t st) {
+    if (B == 0) return hipSuccess;
+    hipLaunchKernelGGL(ocx_gen_seek_kernel, dim3((unsigned)((B + OCX_BLOCK - 1) / OCX_BLOCK)),
+                       dim3(OCX_BLOCK), 0, st, base_seed, T_seed, run0, B, d, st_out, lab_out);
+    return hipGetLastError();
+}
+
+hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const uint64_t* st_in,
+                                   uint64_t* st_out, const uint64_t* lab_in, uint64_t* lab_out,
+                                   double* zt, double* ytl, hipStream_t st) {
+    const int64_t nlanes = L->G * L->S;
+    if (nlanes == 0 || L->T == 0) return hipSuccess;
+    if ((int64_t)L->P * L->C > 64) return hipErrorNotSupported;
+    const unsigned grid = (unsigned)((nlanes + 63) / 64);
+    hipLaunchKernelGGL(ocx_gen_staged_kernel<OCX_FAM_GT>, dim3(grid), dim3(64), 0, st,
+                       (uint64_t)0, L->T, (int64_t)0, L->B, (int)L->d, L->P, L->C, L->G, nullptr,
+                       nullptr, 0.0, zt, ytl, T_seed, st_in, st_out, lab_in, lab_out);
     return hipGetLastError();
 }

@@ -14,98 +14,10 @@
 // butterfly (ocx_seq_sum).
 #include <algorithm>
 
+#include "ocx_device_math.h"
+#include "ocx_dispatch.h"
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
-
-namespace {
-
-template <int C>
-__device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p) {
-#pragma unroll
-    for (int k = 0; k < C / 2; ++k) {
-#if OCX_LOAD_NT
-        dst[k] = __builtin_nontemporal_load(p + k * 64);
-#else
-        dst[k] = p[k * 64];
-#endif
-    }
-}
-
-__device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
-    return (j & 1) ? zb[j >> 1].y : zb[j >> 1].x;
-}
-
-}  // namespace
-
-// ---------------------------------------------------------------------------
-// Per-sequence totals of C per-lane products p[j] (coordinate c*C + j).
-//   tree  (CHAIN=false): lane-local sequential sum, then the P-lane butterfly;
-//   chain (CHAIN=true):  the running sum visits lanes 0..P-1 in order and each
-//         lane adds its products one by one → exactly the reference's sequential
-//         order over all d coordinates (exact mode for d > 64).
-// ---------------------------------------------------------------------------
-template <int C, int P, bool CHAIN>
-__device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
-    if constexpr (!CHAIN || P == 1) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < C; ++j) acc += p[j];
-        return ocx_seq_sum<P>(acc);
-    } else {
-        const int c = lane % P;
-        const int base = lane - c;
-        double acc = 0.0;
-        for (int cc = 0; cc < P; ++cc) {
-            if (c == cc) {
-#pragma unroll
-                for (int j = 0; j < C; ++j) acc += p[j];
-            }
-            acc = __shfl(acc, base + cc, 64);
-        }
-        return acc;
-    }
-}
-
-__device__ __forceinline__ double ocx_grad(double diff) {  // fast_algorithms.py:27-34
-    return diff > 0.0 ? 0.5 : (diff < 0.0 ? -0.5 : 0.0);
-}
-
-// FTRL action (fast_algorithms.py:52-66): x = (s*theta) * f, f = 1/||s*theta|| if > 1
-template <int C, int P, bool CHAIN>
-__device__ __forceinline__ void ocx_action_ftrl(const double (&th)[C], int64_t t1, double eta0,
-                                                double (&x)[C], int lane) {
-    const double sc = -(eta0 / sqrt((double)t1));
-    double p[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) {
-        x[j] = sc * th[j];
-        p[j] = x[j] * x[j];
-    }
-    const double nsq = ocx_total<C, P, CHAIN>(p, lane);
-    const double f = 1.0 / sqrt(nsq > 1.0 ? nsq : 1.0);  // nsq <= 1: f == 1.0 exactly
-#pragma unroll
-    for (int j = 0; j < C; ++j) x[j] *= f;
-}
-
-// FTL action (fast_algorithms.py:37-49): x = -(1/||theta||) * theta, or 0
-template <int C, int P, bool CHAIN>
-__device__ __forceinline__ void ocx_action_ftl(const double (&th)[C], double (&x)[C], int lane) {
-    double p[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
-    const double nsq = ocx_total<C, P, CHAIN>(p, lane);
-    const double sc = -(1.0 / sqrt(nsq));
-#pragma unroll
-    for (int j = 0; j < C; ++j) x[j] = (nsq == 0.0) ? 0.0 : sc * th[j];
-}
-
-template <int C, int P, bool CHAIN>
-__device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
-    double p[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * x[j];
-    return ocx_total<C, P, CHAIN>(p, lane);
-}
 
 // ---------------------------------------------------------------------------
 // fast_algorithms.py:88-115 `_simulate_alg_core` (+ exact_ftl.py:230-277 outputs)
@@ -400,23 +312,7 @@ __global__ void ocx_max_kernel(const double* __restrict__ r, int64_t B, double* 
 // ---------------------------------------------------------------------------
 // Launchers: runtime (C, P) → template instance
 // ---------------------------------------------------------------------------
-// Register-ring depth (steps in flight per wave) by coordinates per lane; tuned on
-// MI355X with tools/tune.py (the -D overrides build the tuning variants).
-#ifndef OCX_NB_LE8
-#define OCX_NB_LE8 4
-#endif
-#ifndef OCX_NB_16
-#define OCX_NB_16 3
-#endif
-#ifndef OCX_NB_GE32
-#define OCX_NB_GE32 2
-#endif
-#ifndef OCX_LOAD_NT
-#define OCX_LOAD_NT 1
-#endif
-
 namespace {
-constexpr int nb_for(int C) { return C <= 8 ? OCX_NB_LE8 : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32); }
 
 inline unsigned grid_for(int64_t G) {
     return (unsigned)((G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK);
@@ -449,56 +345,6 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
     return hipGetLastError();
 }
 
-// (C, P) tree instances for every supported C; chain (exact mode, P > 1) instances for
-// power-of-two C.
-#define OCX_DISPATCH_P(FN, C, ...)                    \
-    switch (L->P) {                                   \
-        case 1: return FN<C, 1, false>(__VA_ARGS__);  \
-        case 2: return FN<C, 2, false>(__VA_ARGS__);  \
-        case 4: return FN<C, 4, false>(__VA_ARGS__);  \
-        case 8: return FN<C, 8, false>(__VA_ARGS__);  \
-        case 16: return FN<C, 16, false>(__VA_ARGS__); \
-        case 32: return FN<C, 32, false>(__VA_ARGS__); \
-        case 64: return FN<C, 64, false>(__VA_ARGS__); \
-        default: return hipErrorInvalidValue;         \
-    }
-
-#define OCX_DISPATCH_CHAIN_P(FN, C, ...)             \
-    switch (L->P) {                                  \
-        case 2: return FN<C, 2, true>(__VA_ARGS__);  \
-        case 4: return FN<C, 4, true>(__VA_ARGS__);  \
-        case 8: return FN<C, 8, true>(__VA_ARGS__);  \
-        case 16: return FN<C, 16, true>(__VA_ARGS__); \
-        case 32: return FN<C, 32, true>(__VA_ARGS__); \
-        case 64: return FN<C, 64, true>(__VA_ARGS__); \
-        default: return hipErrorInvalidValue;        \
-    }
-
-#define OCX_DISPATCH(FN, ...)                                         \
-    if (L->chain) {                                                   \
-        switch (L->C) {                                               \
-            case 2: OCX_DISPATCH_CHAIN_P(FN, 2, __VA_ARGS__)          \
-            case 4: OCX_DISPATCH_CHAIN_P(FN, 4, __VA_ARGS__)          \
-            case 8: OCX_DISPATCH_CHAIN_P(FN, 8, __VA_ARGS__)          \
-            case 16: OCX_DISPATCH_CHAIN_P(FN, 16, __VA_ARGS__)        \
-            case 32: OCX_DISPATCH_CHAIN_P(FN, 32, __VA_ARGS__)        \
-            case 64: OCX_DISPATCH_CHAIN_P(FN, 64, __VA_ARGS__)        \
-            default: return hipErrorInvalidValue;                     \
-        }                                                             \
-    }                                                                 \
-    switch (L->C) {                                                   \
-        case 2: OCX_DISPATCH_P(FN, 2, __VA_ARGS__)                    \
-        case 4: OCX_DISPATCH_P(FN, 4, __VA_ARGS__)                    \
-        case 6: OCX_DISPATCH_P(FN, 6, __VA_ARGS__)                    \
-        case 8: OCX_DISPATCH_P(FN, 8, __VA_ARGS__)                    \
-        case 12: OCX_DISPATCH_P(FN, 12, __VA_ARGS__)                  \
-        case 16: OCX_DISPATCH_P(FN, 16, __VA_ARGS__)                  \
-        case 24: OCX_DISPATCH_P(FN, 24, __VA_ARGS__)                  \
-        case 32: OCX_DISPATCH_P(FN, 32, __VA_ARGS__)                  \
-        case 48: OCX_DISPATCH_P(FN, 48, __VA_ARGS__)                  \
-        case 64: OCX_DISPATCH_P(FN, 64, __VA_ARGS__)                  \
-        default: return hipErrorInvalidValue;                         \
-    }
 }  // namespace
 
 bool ocx_supported_C(int C) {

@@ -22,3 +22,11 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
 hipError_t ocx_launch_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
                                  const uint64_t* stream_ids, double p, int64_t block_len,
                                  double* zt, double* ytl, hipStream_t st);
+hipError_t ocx_launch_gen_seek(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
+                               int64_t d, uint64_t* st_out, uint64_t* lab_out, hipStream_t st);
+hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const uint64_t* st_in,
+                                   uint64_t* st_out, const uint64_t* lab_in, uint64_t* lab_out,
+                                   double* zt, double* ytl, hipStream_t st);
+hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const double* yt,
+                                int64_t t0, int alg_flag, double eta0, int mode, double* theta,
+                                double* cum, double* comp, double* regret, hipStream_t st);

@@ -1,0 +1,127 @@
+// ocx_stream.hip — long-horizon (T-chunked) FTRL/FTL for sweeps whose sequences do not
+// fit in HBM at once (configs[3]: T up to 1e5 with 1e6 runs).
+//
+// The horizon is cut into chunks of Tc steps.  Pass A walks the chunks in order:
+// the generator writes chunk c's rows and labels (resuming each stream from its saved
+// PCG state) and ocx_alg_chunk_kernel advances theta and the cumulative loss, which
+// live in HBM between launches.  Pass B regenerates every chunk from the same saved
+// states and accumulates the comparator loss of FTL(theta_T) (fast_algorithms.py:113-114).
+// The per-step arithmetic is the same ocx_device_math.h code as ocx_alg_kernel, so the
+// regrets are identical to a single-launch run.
+#include "ocx_device_math.h"
+#include "ocx_dispatch.h"
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+// mode 0: loop steps [t0, t0+Tc) of fast_algorithms.py:99-111, theta/cum in & out.
+// mode 1: comparator loss of those steps with x* = FTL(theta_state); when regret_out
+//         is non-null (last chunk) also regret = cum - comp.
+template <int C, int P, bool CHAIN, int NB>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t Tc,
+    int64_t G, int64_t t0, int alg_flag, double eta0, int mode, double* __restrict__ theta_state,
+    int64_t Dp, double* __restrict__ cum_state, double* __restrict__ comp_state,
+    double* __restrict__ regret_out) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const bool live = b < B;
+    const int64_t tstride = 32 * C;
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * Tc * tstride + lane;
+    const double* __restrict__ yp = yt + g * Tc * S + s;
+    double* th_row = theta_state + (live ? b : 0) * Dp + (int64_t)c * C;
+
+    double th[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = live ? th_row[j] : 0.0;
+
+    ocx_d2 zb[NB][K];
+    double yb[NB];
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < Tc) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            yb[u] = yp[u * S];
+        }
+
+    if (mode == 0) {
+        const bool ftl = (alg_flag != 0);
+        double cum = live ? cum_state[b] : 0.0;
+        for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int64_t t = u0 + u;
+                if (t < Tc) {
+                    const int64_t tp = t + NB - 1;
+                    if (tp < Tc) {
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                        yb[(u + NB - 1) % NB] = yp[tp * S];
+                    }
+                    double x[C];
+                    if (!ftl) ocx_action_ftrl<C, P, CHAIN>(th, t0 + t + 1, eta0, x, lane);
+                    else ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
+                    const double diff = q - yb[u];
+                    cum += 0.5 * fabs(diff);
+                    const double gq = ocx_grad(diff);
+#pragma unroll
+                    for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);
+                }
+            }
+        }
+        if (live) {
+#pragma unroll
+            for (int j = 0; j < C; ++j) th_row[j] = th[j];
+            if (c == 0) cum_state[b] = cum;
+        }
+    } else {
+        double xs[C];
+        ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
+        double comp = live ? comp_state[b] : 0.0;
+        for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int64_t t = u0 + u;
+                if (t < Tc) {
+                    const int64_t tp = t + NB - 1;
+                    if (tp < Tc) {
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                        yb[(u + NB - 1) % NB] = yp[tp * S];
+                    }
+                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                    comp += 0.5 * fabs(q - yb[u]);
+                }
+            }
+        }
+        if (live && c == 0) {
+            comp_state[b] = comp;
+            if (regret_out) regret_out[b] = cum_state[b] - comp;
+        }
+    }
+}
+
+namespace {
+template <int C, int P, bool CH>
+hipError_t launch_chunk_cp(const ocx_layout* L, const double* zt, const double* yt, int64_t t0,
+                           int alg_flag, double eta0, int mode, double* th, double* cum,
+                           double* comp, double* reg, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_alg_chunk_kernel<C, P, CH, nb_for(C)>),
+                       dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
+                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode,
+                       th, L->Dp, cum, comp, reg);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const double* yt,
+                                int64_t t0, int alg_flag, double eta0, int mode, double* theta,
+                                double* cum, double* comp, double* regret, hipStream_t st) {
+    if (L->G == 0 || L->T == 0) return hipSuccess;
+    OCX_DISPATCH(launch_chunk_cp, L, zt, yt, t0, alg_flag, eta0, mode, theta, cum, comp, regret,
+                 st)
+}

@@ -301,3 +301,22 @@ def test_driver_stats_golden(ocx, golden):
         for k, (m, c) in rec["stats"].items():
             assert np.array_equal(st[k][0], np.array([F(v) for v in m])), (title, k)
             assert np.array_equal(st[k][1], np.array([F(v) for v in c])), (title, k)
+
+
+# ------------------------------------------------------------------ long-horizon (chunked)
+@pytest.mark.parametrize("T,d,runs,P", [(300, 5, 100, 1), (257, 64, 40, 0), (1000, 16, 70, -1)])
+def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
+    """A tiny HBM budget forces the T-chunked path (seek → pass A → pass B with saved PCG
+    states): regrets must equal the single-launch path bit for bit."""
+    eng = ocx["engine"]
+    whole = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(200e3 / 2**30))  # ~200 KB → many chunks
+    chunked = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
+    assert np.array_equal(whole, chunked)
+    for r in (0, runs - 1):
+        z, y = O.gT_sample(4, T, 7 + r, d)
+        ref = O.simulate_alg(z, y, 0, SQ2)
+        if P == 0:
+            assert close(chunked[r], ref)
+        else:
+            assert chunked[r] == ref

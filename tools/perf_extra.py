@@ -1,0 +1,93 @@
+"""Secondary measurements on one MI355X (one JSON line each; not the bench contract).
+
+  gen      generator throughput (d=64 g(T) rows) at several batch sizes
+  sweep    configs[3]-style g(T) sweep per T, generation included (runs scaled down)
+  driver   fast_driver.main() on device (g(T) runs=1000 + the four cases, full sizes)
+  smart    SMART kernel throughput (d=5, T=1000, 768 sequences)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def sync():
+    import torch
+    torch.cuda.synchronize()
+
+
+def gen(args):
+    import torch
+    from online_convex_optimization_amd import engine
+    for B, T in ((32768, 10000), (131072, 2000), (262144, 1000)):
+        db = engine.DeviceBatch(B, T, 64, lanes_per_seq=1)
+        db.generate_gT(0, 0)
+        sync()
+        t0 = time.perf_counter()
+        db.generate_gT(0, 0)
+        sync()
+        tg = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        db.simulate_alg()
+        sync()
+        ts = time.perf_counter() - t0
+        print(json.dumps({"what": "gen", "B": B, "T": T, "d": 64, "gen_s": tg,
+                          "normals_per_s": B * T * 64 / tg, "gen_timesteps_per_s": B * T / tg,
+                          "sim_s": ts, "gen+sim_timesteps_per_s": B * T / (tg + ts)}), flush=True)
+        del db
+        torch.cuda.empty_cache()
+
+
+def sweep(args):
+    from online_convex_optimization_amd import engine
+    for T, runs in ((100, 100000), (1000, 100000), (10000, 20000)):
+        engine.gT_regrets(T, 64, d=64, lanes_per_seq=1)  # warm
+        t0 = time.perf_counter()
+        regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64, "seconds": dt,
+                          "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
+              flush=True)
+
+
+def driver(args):
+    from online_convex_optimization_amd import drivers
+    t0 = time.perf_counter()
+    g_emp, stats = drivers.fast_driver_main()
+    dt = time.perf_counter() - t0
+    out = {"what": "fast_driver_main", "seconds": dt,
+           "g_emp": [g_emp[T] for T in range(100, 1100, 100)],
+           "T1000": {title: {k: float(st[k][0][-1]) for k in st} for title, st in stats.items()}}
+    print(json.dumps(out), flush=True)
+
+
+def smart(args):
+    from online_convex_optimization_amd import engine
+    import torch
+    B, T = 768, 1000
+    db = engine.DeviceBatch(B, T, 5, lanes_per_seq=1)
+    db.generate_family("iid", 2025 * (1 + np.repeat(np.arange(48), 16)),
+                       13 + np.tile(np.arange(16), 48))
+    db.simulate_smart(math.sqrt(2 * T))
+    sync()
+    t0 = time.perf_counter()
+    db.simulate_smart(math.sqrt(2 * T))
+    sync()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"what": "smart", "B": B, "T": T, "d": 5, "seconds": dt,
+                      "timesteps_per_s": B * T / dt}), flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="+", choices=["gen", "sweep", "driver", "smart"])
+    a = ap.parse_args()
+    for w in a.what:
+        globals()[w](a)
