@@ -47,7 +47,7 @@ def gen(args):
 
 def sweep(args):
     from online_convex_optimization_amd import engine
-    for T, runs in ((100, 100000), (1000, 100000), (10000, 20000)):
+    for T, runs in ((100, 1000000), (1000, 1000000), (10000, 131072), (100000, 131072)):
         engine.gT_regrets(T, 64, d=64, lanes_per_seq=1)  # warm
         t0 = time.perf_counter()
         regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
