@@ -46,13 +46,15 @@ typedef enum ocx_status {
     OCX_E_UNSUPPORTED = -3
 } ocx_status;
 
-/* Tiled HBM layout shared by the generator and the simulation kernels.
+/* Tiled HBM layout shared by the generators and the simulation kernels.
  * A wave-group is 64 lanes = S sequences x P lanes; lane L = s*P + c owns
- * coordinates [c*C, (c+1)*C) of sequence g*S + s.  For group g and step t the
- * z tile is 64*C contiguous doubles stored [k = 0..C/2-1][lane 0..63][2], so one
- * wave loads a step with C/2 fully coalesced 1 KiB dwordx4 instructions.
- *   z_tiled[((g*T + t)*64*C) + k*128 + L*2 + e] = z[b][t][c*C + 2k + e]
- *   y_tiled[(g*T + t)*S + s]                   = y[b][t]
+ * coordinates [c*C, (c+1)*C) of sequence b = g*S + s.  Coordinate pair k of every
+ * lane lives in "plane" k (k < C/2): per (g, t) one contiguous 1 KiB row
+ * [lane 0..63][2].  A wave therefore streams C/2 independent contiguous regions
+ * (one per plane) with fully coalesced 1 KiB dwordx4 loads, which keeps more HBM
+ * streams open than one region per wave:
+ *   z_tiled[((k*G + g)*T + t)*128 + L*2 + e] = z[b][t][c*C + 2k + e]
+ *   y_tiled[(g*T + t)*S + s]                 = y[b][t]
  * Padding (coordinates j >= d, sequences b >= B) holds zeros. */
 typedef struct ocx_layout {
     int64_t B, T, d;  /* logical sizes */

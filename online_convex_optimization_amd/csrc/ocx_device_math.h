@@ -22,13 +22,15 @@
 constexpr int nb_for(int C) { return C <= 8 ? OCX_NB_LE8 : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32); }
 
 template <int C>
-__device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p) {
+__device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p,
+                                              int64_t kst) {
+    // pair k of this lane's step lives in plane k, kst = G*T*64 ocx_d2 further on
 #pragma unroll
     for (int k = 0; k < C / 2; ++k) {
 #if OCX_LOAD_NT
-        dst[k] = __builtin_nontemporal_load(p + k * 64);
+        dst[k] = __builtin_nontemporal_load(p + k * kst);
 #else
-        dst[k] = p[k * 64];
+        dst[k] = p[k * kst];
 #endif
     }
 }

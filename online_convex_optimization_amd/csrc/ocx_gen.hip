@@ -157,7 +157,7 @@ __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
     }
     ocx_pw_plan plan;
     ocx_pw_build(&plan, d);
-    const int64_t tile = 64 * (int64_t)C;
+    const int64_t kst = G * T * 64;  // plane stride in ocx_d2 (pair k of a step)
     const int64_t g0 = seq0 / S;  // first group of this wave
     const int64_t gb = b / S;
     double* yrow = ytl + gb * T * S + (b - gb * S);
@@ -191,10 +191,10 @@ __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
             const int sl = gi * S + lane / P;  // wave-local sequence of this lane's slot
             const int c = lane % P;
             const double* src = rows + sl * OCX_GEN_ROW + c * C;
-            ocx_d2* dst = reinterpret_cast<ocx_d2*>(zt + (g * T + t) * tile) + lane;
+            ocx_d2* dst = reinterpret_cast<ocx_d2*>(zt) + (g * T + t) * 64 + lane;
             for (int k = 0; k < C / 2; ++k)
                 __builtin_nontemporal_store(*reinterpret_cast<const ocx_d2*>(src + 2 * k),
-                                            dst + k * 64);
+                                            dst + k * kst);
         }
         __syncthreads();
     }
@@ -219,16 +219,17 @@ __global__ __launch_bounds__(64) void ocx_gen_staged_kernel(
 
 // Label flips / switching leaders (sequence_generation.py:24-47): z = e1, y patterned.
 __global__ void ocx_gen_fixed_kernel(int family, int64_t block_len, int64_t B, int64_t T,
-                                     int P, int C, int64_t zn, int64_t yn,
+                                     int P, int C, int64_t G, int64_t zn, int64_t yn,
                                      double* __restrict__ zt, double* __restrict__ ytl) {
     const int S = 64 / P;
-    const int64_t tile = 64 * (int64_t)C;
     for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < zn;
          o += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t tix = o / tile;
-        const int r = (int)(o - tix * tile);
-        const int k = r >> 7, L = (r & 127) >> 1, e = r & 1;
-        const int64_t b = (tix / T) * S + L / P;
+        // o = ((k*G + g)*T + t)*128 + 2L + e
+        const int64_t row = o >> 7;
+        const int L = (int)((o & 127) >> 1), e = (int)(o & 1);
+        const int64_t kg = row / T;
+        const int64_t k = kg / G, g = kg - k * G;
+        const int64_t b = g * S + L / P;
         const int64_t j = (int64_t)(L % P) * C + 2 * k + e;
         zt[o] = (b < B && j == 0) ? 1.0 : 0.0;
     }
@@ -291,13 +292,13 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_gen_regen_kernel(
     const int S = 64 / P;
     const int64_t g = b / S;
     const int s = (int)(b - g * S);
-    const int64_t tile = 64 * (int64_t)C;
     const int64_t Dp = (int64_t)P * C;
+    const int64_t G = nlanes / S;
     auto zidx = [&](int64_t t, int64_t j) -> int64_t {
         const int c = (int)(j / C);
         const int r = (int)(j - (int64_t)c * C);
         const int L = s * P + c;
-        return (g * T + t) * tile + (r >> 1) * 128 + L * 2 + (r & 1);
+        return (((int64_t)(r >> 1) * G + g) * T + t) * 128 + L * 2 + (r & 1);
     };
     double* yrow = ytl + g * T * S + s;
 
@@ -353,7 +354,7 @@ hipError_t ocx_launch_gen_family(const ocx_layout* L, int family, const uint64_t
         const int64_t n = std::max(L->z_elems, L->y_elems);
         const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
         hipLaunchKernelGGL(ocx_gen_fixed_kernel, dim3(grid), dim3(256), 0, st, family, block_len,
-                           L->B, L->T, L->P, L->C, L->z_elems, L->y_elems, zt, ytl);
+                           L->B, L->T, L->P, L->C, L->G, L->z_elems, L->y_elems, zt, ytl);
         return hipGetLastError();
     }
     if ((int64_t)L->P * L->C > 64) return hipErrorNotSupported;

@@ -36,8 +36,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
-    const int64_t tstride = 32 * C;  // ocx_d2 per step tile
+    const int64_t tstride = 64;  // ocx_d2 per step within a plane
     const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;  // plane stride (pairs k)
     const double* __restrict__ yp = yt + g * T * S + s;
     const bool ftl = (alg_flag != 0);
 
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u)
         if (u < T) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
             yb[u] = yp[u * S];
         }
 
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
             if (t < T) {
                 const int64_t tp = t + NB - 1;
                 if (tp < T) {
-                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                     yb[(u + NB - 1) % NB] = yp[tp * S];
                 }
                 double x[C];
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u)
         if (u < T) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
             yb[u] = yp[u * S];
         }
     double comp = 0.0;
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
             if (t < T) {
                 const int64_t tp = t + NB - 1;
                 if (tp < T) {
-                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                     yb[(u + NB - 1) % NB] = yp[tp * S];
                 }
                 const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
@@ -144,8 +145,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
-    const int64_t tstride = 32 * C;
+    const int64_t tstride = 64;  // ocx_d2 per step within a plane
     const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;  // plane stride (pairs k)
     const double* __restrict__ yp = yt + g * T * S + s;
     const double th_sw = (b < B) ? thresh[b] : 0.0;
 
@@ -158,7 +160,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
 
     for (int64_t t = 0; t < T; ++t) {
         ocx_d2 z[K];
-        ocx_load_tile<C>(z, zp + t * tstride);
+        ocx_load_tile<C>(z, zp + t * tstride, kst);
         const double yv = yp[t * S];
         // FTL is always run and updated (:140-146)
         double x[C];
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
             double s_loss = 0.0;
             for (int64_t i = 0; i <= t; ++i) {
                 ocx_d2 zi[K];
-                ocx_load_tile<C>(zi, zp + i * tstride);
+                ocx_load_tile<C>(zi, zp + i * tstride, kst);
                 const double q = ocx_zdot<C, P, CHAIN>(zi, sv, lane);
                 s_loss += 0.5 * fabs(q - yp[i * S]);
             }
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
     double comp = 0.0;
     for (int64_t t = 0; t < T; ++t) {
         ocx_d2 z[K];
-        ocx_load_tile<C>(z, zp + t * tstride);
+        ocx_load_tile<C>(z, zp + t * tstride, kst);
         const double q = ocx_zdot<C, P, CHAIN>(z, sv, lane);
         comp += 0.5 * fabs(q - yp[t * S]);
     }
@@ -228,23 +230,25 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
-    const int64_t tstride = 32 * C;
+    const int64_t tstride = 64;  // ocx_d2 per step within a plane
     const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;  // plane stride (pairs k)
     const ocx_d2* __restrict__ ap =
         reinterpret_cast<const ocx_d2*>(at) + g * (T + 1) * tstride + lane;
+    const int64_t kst_a = G * (T + 1) * 64;
     const double* __restrict__ yp = yt + g * T * S + s;
     double aT[C];
     {
         ocx_d2 a2[K];
-        ocx_load_tile<C>(a2, ap + T * tstride);
+        ocx_load_tile<C>(a2, ap + T * tstride, kst_a);
 #pragma unroll
         for (int j = 0; j < C; ++j) aT[j] = ocx_zj(a2, j);
     }
     double cum = 0.0, comp = 0.0;
     for (int64_t t = 0; t < T; ++t) {
         ocx_d2 z[K], a2[K];
-        ocx_load_tile<C>(z, zp + t * tstride);
-        ocx_load_tile<C>(a2, ap + t * tstride);
+        ocx_load_tile<C>(z, zp + t * tstride, kst);
+        ocx_load_tile<C>(a2, ap + t * tstride, kst_a);
         const double yv = yp[t * S];
         double a[C];
 #pragma unroll
@@ -264,15 +268,17 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
 // Layout packing and small reductions
 // ---------------------------------------------------------------------------
 __global__ void ocx_pack_z_kernel(const double* __restrict__ z, double* __restrict__ zt,
-                                  int64_t B, int64_t T, int64_t d, int P, int C, int64_t total) {
+                                  int64_t B, int64_t T, int64_t d, int P, int C, int64_t G,
+                                  int64_t total) {
     const int S = 64 / P;
-    const int64_t tile = 64 * (int64_t)C;
     for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total;
          o += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t tix = o / tile;
-        const int r = (int)(o - tix * tile);
-        const int k = r >> 7, L = (r & 127) >> 1, e = r & 1;
-        const int64_t g = tix / T, t = tix - (tix / T) * T;
+        // o = ((k*G + g)*T + t)*128 + 2L + e
+        const int64_t row = o >> 7;
+        const int L = (int)((o & 127) >> 1), e = (int)(o & 1);
+        const int64_t kg = row / T;
+        const int64_t t = row - kg * T;
+        const int64_t k = kg / G, g = kg - k * G;
         const int64_t b = g * S + L / P;
         const int64_t j = (int64_t)(L % P) * C + 2 * k + e;
         zt[o] = (b < B && j < d) ? z[(b * T + t) * d + j] : 0.0;
@@ -377,7 +383,7 @@ hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y
     if (zn > 0) {
         const unsigned grid = (unsigned)std::min<int64_t>((zn + 255) / 256, 65536);
         hipLaunchKernelGGL(ocx_pack_z_kernel, dim3(grid), dim3(256), 0, st, z, zt, L->B, L->T,
-                           L->d, L->P, L->C, zn);
+                           L->d, L->P, L->C, L->G, zn);
     }
     if (yn > 0) {
         const unsigned grid = (unsigned)std::min<int64_t>((yn + 255) / 256, 65536);

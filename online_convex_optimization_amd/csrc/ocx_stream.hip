@@ -31,8 +31,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
     const int c = lane % P;
     const int64_t b = g * S + s;
     const bool live = b < B;
-    const int64_t tstride = 32 * C;
+    const int64_t tstride = 64;  // ocx_d2 per step within a plane
     const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * Tc * tstride + lane;
+    const int64_t kst = G * Tc * 64;  // plane stride (pairs k)
     const double* __restrict__ yp = yt + g * Tc * S + s;
     double* th_row = theta_state + (live ? b : 0) * Dp + (int64_t)c * C;
 
@@ -45,7 +46,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u)
         if (u < Tc) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride);
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
             yb[u] = yp[u * S];
         }
 
@@ -59,7 +60,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                 if (t < Tc) {
                     const int64_t tp = t + NB - 1;
                     if (tp < Tc) {
-                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                         yb[(u + NB - 1) % NB] = yp[tp * S];
                     }
                     double x[C];
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                 if (t < Tc) {
                     const int64_t tp = t + NB - 1;
                     if (tp < Tc) {
-                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride);
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                         yb[(u + NB - 1) % NB] = yp[tp * S];
                     }
                     const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);

@@ -3,12 +3,11 @@ import numpy as np
 
 
 def untile_z(zt: np.ndarray, L) -> np.ndarray:
-    """z_tiled (flat, G*T*64*C) → z [B, T, d]."""
+    """z_tiled (flat, (C/2)*G*T*128) → z [B, T, d]."""
     G, T, C, P, S = L.G, L.T, L.C, L.P, L.S
-    a = zt.reshape(G, T, C // 2, 64, 2)            # [g][t][k][lane][e]
-    a = a.reshape(G, T, C // 2, S, P, 2)            # lane = s*P + c
-    a = a.transpose(0, 3, 1, 4, 2, 5)               # [g][s][t][c][k][e]
-    a = a.reshape(G * S, T, P * C)                  # j = c*C + 2k + e
+    a = zt.reshape(C // 2, G, T, S, P, 2)      # [k][g][t][s][c][e], lane = s*P + c
+    a = a.transpose(1, 3, 2, 4, 0, 5)           # [g][s][t][c][k][e]
+    a = a.reshape(G * S, T, P * C)              # j = c*C + 2k + e
     return a[:L.B, :, :L.d]
 
 

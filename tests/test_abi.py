@@ -72,7 +72,7 @@ def test_auto_layout_choices():
 
 
 def test_untile_roundtrip_matches_pack_formula():
-    # host restatement of ocx_pack_z_kernel's index map, inverted by untile_z
+    # host restatement of ocx_pack_z_kernel's plane-major index map, inverted by untile_z
     B, T, d = 37, 5, 11
     for P in (1, 2, 4, 8, 64):
         L = _lib.layout(B, T, d, P)
@@ -81,10 +81,9 @@ def test_untile_roundtrip_matches_pack_formula():
         y = rng.standard_normal((B, T))
         zt = np.zeros(L.z_elems)
         o = np.arange(L.z_elems)
-        tile = 64 * L.C
-        tix, r = o // tile, o % tile
-        k, lane, e = r >> 7, (r & 127) >> 1, r & 1
-        g, t = tix // T, tix % T
+        row, lane, e = o >> 7, (o & 127) >> 1, o & 1
+        kg, t = row // T, row % T
+        k, g = kg // L.G, kg % L.G
         b = g * L.S + lane // L.P
         j = (lane % L.P) * L.C + 2 * k + e
         ok = (b < B) & (j < d)

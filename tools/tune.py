@@ -88,12 +88,14 @@ def main():
         lib = ctypes.CDLL(build_probe())
         out = torch.zeros(1 << 20, dtype=torch.float64, device="cuda")
         nbytes = db.z_bytes
-        for kind, nw in ((0, 2048), (0, 4096), (0, 8192), (1, 0)):
+        for kind, nw in ((0, 2048), (0, 4096), (0, 8192), (0, 16384), (1, 0), (2, 2048),
+                         (2, 4096), (2, 8192), (3, 2048), (3, 4096), (4, 4096), (4, 8192)):
             ms = timeit(lambda: lib.probe_run(kind, ctypes.c_void_p(db.z.data_ptr()),
                                               ctypes.c_int64(nbytes), ctypes.c_int64(nw),
                                               ctypes.c_void_p(out.data_ptr()),
                                               ctypes.c_void_p(st.cuda_stream)), st)
-            print(json.dumps({"what": "probe", "kind": ["region", "stride"][kind], "waves": nw,
+            print(json.dumps({"what": "probe", "kind": ["region8", "stride", "region16", "region32",
+                                                        "region16plain"][kind], "waves": nw,
                               "bytes": nbytes, "ms": ms, "GBs": nbytes / ms / 1e6}), flush=True)
 
 
