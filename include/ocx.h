@@ -94,6 +94,18 @@ int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_
                              const double* thresh, double eta0, double* regret,
                              int64_t* switch_step, int lanes_per_seq, int device);
 
+/* exact_ftl.py:423-453 run_ftl_exact (compute_prefix_actions :280-303 + replay
+ * :306-333) for the l2 ball (norm must be 0), batched, in the closed form that is exact
+ * when every ||z_t|| <= 1 and y_t = ±1: the prefix minimiser of ½Σ|z_i·x − y_i| over the
+ * ball is S_t/||S_t|| (0 if S_t = 0), S_t = Σ_{i<t} y_i z_i.  regime [B] (int32, 1 = the
+ * data were in that regime, within 1e-6 on ||z_t||²); outside it the returned numbers
+ * are not the SOCP solution and callers must reject them.  cmp_action [B][d] nullable
+ * = actions[T] (the exact comparator of the whole sequence).  The reference solves an
+ * SOCP with cvxpy, absent here: parity unpinned. */
+int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                        int norm, double* cum_loss, double* comp_loss, double* cmp_action,
+                        int32_t* regime, int lanes_per_seq, int device);
+
 /* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
  * cum_loss = sum_{t<T} 0.5|z_t.a_t - y_t|; comp_loss = sum_t 0.5|z_t.a_T - y_t|. */
 int ocx_replay_batch(const double* z, const double* y, const double* actions, int64_t B,
@@ -135,6 +147,11 @@ int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seed
 int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                          int alg_flag, double eta0, const double* comparator, double* regret,
                          double* cum_loss, double* comp_loss, double* x_last, void* stream);
+
+/* ocx_ftl_exact_batch on device (norm 0 = l2 only). */
+int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
+                      double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
+                      void* stream);
 
 /* fast_algorithms.py:118-164 on device; thresh [B] device. */
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,

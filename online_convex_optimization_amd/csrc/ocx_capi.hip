@@ -222,8 +222,20 @@ int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const doubl
                          double* cum_loss, double* comp_loss, double* x_last, void* stream) {
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
-    OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag, eta0, comparator, regret, cum_loss,
-                           comp_loss, x_last, (hipStream_t)stream));
+    OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag != 0 ? 1 : 0, eta0, comparator, regret,
+                           cum_loss, comp_loss, x_last, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
+                      double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
+                      void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (L->B && !regime) return fail(OCX_E_INVALID, "regime output is required");
+    OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, 2, 0.0, nullptr, nullptr, cum_loss, comp_loss,
+                           nullptr, (hipStream_t)stream, cmp_action, regime));
     return OCX_OK;
 }
 
@@ -292,8 +304,8 @@ int ocx_simulate_alg_batch(const double* z, const double* y, int64_t B, int64_t 
     double* o = cx->out.as<double>();
     double* dxl = x_last ? o + 3 * B : nullptr;
     if (dxl && B * d) OCX_HIP(hipMemsetAsync(dxl, 0, (size_t)B * d * 8, st));
-    OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), alg_flag, eta0, dcmp, o,
-                           o + B, o + 2 * B, dxl, st));
+    OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), alg_flag != 0 ? 1 : 0,
+                           eta0, dcmp, o, o + B, o + 2 * B, dxl, st));
     std::vector<double> h((size_t)B * (3 + (x_last ? d : 0)));
     OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipStreamSynchronize(st));
@@ -335,6 +347,42 @@ int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_
     if (switch_step)
         OCX_HIP(hipMemcpyAsync(switch_step, cx->sw.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
+int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                        int norm, double* cum_loss, double* comp_loss, double* cmp_action,
+                        int32_t* regime, int lanes_per_seq, int device) {
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || !regime) return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * (2 + d) * 8 + (size_t)B * 4));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    double* o = cx->out.as<double>();
+    int* rg = reinterpret_cast<int*>(o + B * (2 + d));
+    OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 2, 0.0, nullptr, nullptr,
+                           o, o + B, nullptr, st, o + 2 * B, rg));
+    std::vector<double> h((size_t)B * (2 + d));
+    OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    if (cum_loss) std::memcpy(cum_loss, h.data(), B * 8);
+    if (comp_loss) std::memcpy(comp_loss, h.data() + B, B * 8);
+    if (cmp_action && d) std::memcpy(cmp_action, h.data() + 2 * B, (size_t)B * d * 8);
     return OCX_OK;
 }
 

@@ -21,13 +21,21 @@
 
 // ---------------------------------------------------------------------------
 // fast_algorithms.py:88-115 `_simulate_alg_core` (+ exact_ftl.py:230-277 outputs)
+//   algo 0 FTRL, 1 FTL (the reference's alg_flag 0 / non-zero);
+//   algo 2 exact FTL over the l2 ball (exact_ftl.py:280-333 compute_prefix_actions +
+//          replay) in its linear regime: when every ||z_t|| <= 1 and y_t = ±1,
+//          ½Σ|z_i·x − y_i| = ½(t − x·S_t) on the ball, so the prefix minimiser is
+//          S_t/||S_t|| (0 if S_t = 0) with S_t = Σ_{i<t} y_i z_i — the FTL action of
+//          theta = −S_t.  regime_out[b] reports whether the data were in that regime
+//          (max ||z_t||² <= 1 + 1e-6 and |y_t| == 1); the caller rejects otherwise.
+// cmp_out [B][d] (nullable) receives the comparator action of the second pass.
 // ---------------------------------------------------------------------------
 template <int C, int P, bool CHAIN, int NB>
 __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
-    int64_t d, int64_t G, int alg_flag, double eta0, const double* __restrict__ comparator,
+    int64_t d, int64_t G, int algo, double eta0, const double* __restrict__ comparator,
     double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
-    double* __restrict__ x_last) {
+    double* __restrict__ x_last, double* __restrict__ cmp_out, int* __restrict__ regime_out) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -40,7 +48,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
     const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
     const int64_t kst = G * T * 64;  // plane stride (pairs k)
     const double* __restrict__ yp = yt + g * T * S + s;
-    const bool ftl = (alg_flag != 0);
+    const bool ftl = (algo != 0);
+    const bool exact = (algo == 2);
+    bool linear = true;  // algo 2: data inside the closed form's regime so far
 
     double th[C];
 #pragma unroll
@@ -79,7 +89,15 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
                 }
                 const double diff = q - yb[u];  // :106-111
                 cum += 0.5 * fabs(diff);
-                const double gq = ocx_grad(diff);
+                double gq = ocx_grad(diff);
+                if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
+                    double p[C];
+#pragma unroll
+                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * ocx_zj(zb[u], j);
+                    const double zz = ocx_total<C, P, CHAIN>(p, lane);
+                    linear = linear && zz <= 1.0 + 1e-6 && fabs(yb[u]) == 1.0;
+                    gq = -yb[u];
+                }
 #pragma unroll
                 for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);  // gq*z is exact
             }
@@ -96,6 +114,13 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
         }
     } else {
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
+    }
+    if (cmp_out != nullptr && b < B) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            const int64_t jj = (int64_t)c * C + j;
+            if (jj < d) cmp_out[b * d + jj] = xs[j];
+        }
     }
 
     // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
@@ -126,6 +151,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
         if (regret) regret[b] = cum - comp;
         if (cum_out) cum_out[b] = cum;
         if (comp_out) comp_out[b] = comp;
+        if (regime_out) regime_out[b] = linear ? 1 : 0;
     }
 }
 
@@ -325,12 +351,12 @@ inline unsigned grid_for(int64_t G) {
 }
 
 template <int C, int P, bool CH>
-hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int algo,
                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                         double* xl, hipStream_t st) {
+                         double* xl, double* cmp_out, int* regime, hipStream_t st) {
     hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C)>), dim3(grid_for(L->G)),
-                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, alg_flag, eta0,
-                       cmp, reg, cum, comp, xl);
+                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, algo, eta0, cmp,
+                       reg, cum, comp, xl, cmp_out, regime);
     return hipGetLastError();
 }
 
@@ -358,11 +384,12 @@ bool ocx_supported_C(int C) {
            C == 48 || C == 64;
 }
 
-hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                          double* xl, hipStream_t st) {
+                          double* xl, hipStream_t st, double* cmp_out, int* regime) {
     if (L->G == 0) return hipSuccess;
-    OCX_DISPATCH(launch_alg_cp, L, zt, yt, alg_flag, eta0, cmp, reg, cum, comp, xl, st)
+    OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
+                 st)
 }
 
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,

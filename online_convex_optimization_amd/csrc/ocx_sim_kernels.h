@@ -6,9 +6,11 @@
 #include "../../include/ocx.h"
 
 bool ocx_supported_C(int C);
-hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int alg_flag,
+// algo: 0 FTRL, 1 FTL, 2 exact FTL (l2 ball, linear regime; see ocx_sim.hip)
+hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                          double* xl, hipStream_t st);
+                          double* xl, hipStream_t st, double* cmp_out = nullptr,
+                          int* regime = nullptr);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

@@ -1,4 +1,5 @@
-"""Batched, device-resident versions of the reference's experiment sweeps.
+"""Batched, device-resident versions of the reference's experiment sweeps
+(fast_driver.py and exact_ftl_driver.py).
 
 ``evaluate_stream_with_stats`` (fast_driver.py:71-127) calls simulate_alg / SMART
 once per (run, T, replicate) on host-built sequences.  Here every (run, replicate)
@@ -105,3 +106,89 @@ def fast_driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 10
             title, T_grid, g_emp, runs=runs_by_title.get(title, 1),
             replicates=replicates_by_title.get(title, 1), base_seed=base_seed, device=device)
     return g_emp, stats
+
+
+# ---------------------------------------------------------------------------
+# exact_ftl_driver.py: FTRL against the exact comparator, exact FTL replay
+# ---------------------------------------------------------------------------
+EXACT_ALGOS = ("FTRL", "FTL (exact)")
+
+
+def exact_case_regrets(title: str, T: int, *, runs: int, replicates: int, base_seed: int = 0,
+                       d: int = 5, p: float = 0.10, block_len: int = 20, lanes_per_seq: int = 1,
+                       device: int = 0) -> Dict[str, np.ndarray]:
+    """exact_ftl_driver.py:157-186 for every (run, rep) of one case and T on device:
+    exact FTL prefix actions (closed form, l2) replayed → "FTL (exact)" regret; FTRL
+    (eta0 = sqrt 2) against actions[T] → "FTRL" regret."""
+    import torch
+    family, stream0 = CASE_FAMILIES[title]
+    B = runs * replicates
+    db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes_per_seq, device=device)
+    run_idx = np.repeat(np.arange(runs), replicates)
+    rep_idx = np.tile(np.arange(replicates), runs)
+    db.generate_family(family, base_seed + 2025 * (run_idx + 1), stream0 + rep_idx, p=p,
+                       block_len=block_len)
+    return _exact_pair(db, B, d, torch)
+
+
+def _exact_pair(db, B, d, torch) -> Dict[str, np.ndarray]:
+    act = torch.zeros((max(B, 1), d), dtype=torch.float64, device=db.device)
+    regime = db.ftl_exact(cmp_action=act)
+    ftl = (db.cum - db.comp).clone()
+    if not bool(regime[:B].all()):
+        raise NotImplementedError("a sequence left the exact-FTL closed form's regime")
+    ftrl = db.simulate_alg(0, SQRT2, comparator=act).clone()
+    return {"FTRL": ftrl[:B].cpu().numpy(), "FTL (exact)": ftl[:B].cpu().numpy()}
+
+
+def exact_evaluate_stream_with_stats(title: str, T_grid: Sequence[int], *, runs: int,
+                                     replicates: int, base_seed: int = 0, device: int = 0) -> Stats:
+    """exact_ftl_driver.py:120-206 for the CASES entry ``title``."""
+    by_T = {k: [[] for _ in range(len(T_grid))] for k in EXACT_ALGOS}
+    per_T = []
+    for T in T_grid:
+        r = exact_case_regrets(title, int(T), runs=runs, replicates=replicates,
+                               base_seed=base_seed, device=device)
+        per_T.append({k: v.reshape(runs, replicates) for k, v in r.items()})
+    for run in range(runs):
+        for ti in range(len(T_grid)):
+            for k in EXACT_ALGOS:
+                by_T[k][ti].append(float(np.mean(list(per_T[ti][k][run]))))
+    stats: Stats = {}
+    for k in EXACT_ALGOS:
+        means, cis = [], []
+        for vals in by_T[k]:
+            arr = np.asarray(vals, dtype=float)
+            means.append(float(np.mean(arr)) if arr.size else 0.0)
+            cis.append(CI_Z * _sem(arr) if arr.size > 1 else 0.0)
+        stats[k] = (np.array(means, dtype=float), np.array(cis, dtype=float))
+    return stats
+
+
+def exact_empirical_worst_case_thresholds(T_grid: Sequence[int], *, runs: int = 200,
+                                          base_seed: int = 0, d: int = 5,
+                                          device: int = 0) -> Dict[int, float]:
+    """exact_ftl_driver.py:64-117: max over runs of FTRL's regret against the exact
+    comparator, on the g(T) adversary regenerated on device."""
+    import torch
+    g = {}
+    for T in T_grid:
+        T = int(T)
+        db = engine.DeviceBatch(runs, T, d, lanes_per_seq=1, device=device)
+        db.generate_gT(base_seed, 0)
+        r = _exact_pair(db, runs, d, torch)["FTRL"]
+        g[T] = engine.max_regret(r)
+    return g
+
+
+def exact_ftl_driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 200,
+                          base_seed: int = 0, device: int = 0):
+    """exact_ftl_driver.py:268-293 minus the figures: (g_emp, stats_by_case)."""
+    T_grid = list(range(100, 1100, 100)) if T_grid is None else [int(t) for t in T_grid]
+    g = exact_empirical_worst_case_thresholds(T_grid, runs=g_runs, base_seed=base_seed,
+                                              device=device)
+    stats = {t: exact_evaluate_stream_with_stats(t, T_grid, runs=RUNS_BY_TITLE.get(t, 1),
+                                                 replicates=REPLICATES_BY_TITLE.get(t, 1),
+                                                 base_seed=base_seed, device=device)
+             for t in CASE_FAMILIES}
+    return g, stats

@@ -91,6 +91,39 @@ def replay_batch(z, y, actions, *, device: int = 0):
     return cum, comp
 
 
+NORMS = {"l2": 0}
+
+
+def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: int = 0,
+                    check_regime: bool = True):
+    """exact_ftl.py:280-333 (compute_prefix_actions + replay) for B sequences on the GPU,
+    in the closed form that is the exact SOCP solution when every ||z_t|| <= 1 and
+    y_t = ±1 (include/ocx.h, ocx_ftl_exact_batch).
+
+    Returns (cum_loss [B], comp_loss [B], comparator actions[T] [B, d], in_regime [B]);
+    with ``check_regime`` a sequence outside the regime raises NotImplementedError (the
+    general SOCP is out of scope: cvxpy is absent and its results are unpinned)."""
+    if norm not in NORMS:
+        raise NotImplementedError(f"exact FTL for norm={norm!r}: only 'l2' is provided")
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    cum = np.zeros(B)
+    comp = np.zeros(B)
+    act = np.zeros((B, d))
+    rg = np.zeros(B, dtype=np.int32)
+    _lib.call("ocx_ftl_exact_batch", ptr(z), ptr(y), B, T, d, NORMS[norm], ptr(cum), ptr(comp),
+              ptr(act), rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq),
+              int(device))
+    ok = rg.astype(bool)
+    if check_regime and not ok.all():
+        bad = int(np.flatnonzero(~ok)[0])
+        raise NotImplementedError(
+            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
+            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+    return cum, comp, act, ok
+
+
 def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
                run0: int = 0, lanes_per_seq: int = 0, device: int = 0) -> np.ndarray:
     """Regrets of FTRL on _rng(base_seed, T, run) sequences, run in [run0, run0+runs),
@@ -234,6 +267,20 @@ class DeviceBatch:
                   th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, self._sp)
         self._keep_th = th
         return self.regret
+
+    def ftl_exact(self, cmp_action=None, regime=None):
+        """Exact FTL (l2 ball, closed form; see ftl_exact_batch) on the resident batch:
+        self.cum / self.comp get the replay and comparator losses, ``cmp_action``
+        [B, d] (device, optional) the exact comparator, ``regime`` [B] int32 the
+        regime flags (allocated when None).  Returns regime."""
+        torch = self.torch
+        if regime is None:
+            regime = torch.zeros(max(self.L.B, 1), dtype=torch.int32, device=self.device)
+        _lib.call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(), 0,
+                  self.cum.data_ptr(), self.comp.data_ptr(),
+                  cmp_action.data_ptr() if cmp_action is not None else None,
+                  regime.data_ptr(), self._sp)
+        return regime
 
     def max_regret(self, out=None):
         torch = self.torch

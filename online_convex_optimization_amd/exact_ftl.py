@@ -4,12 +4,15 @@ Same names and signatures for ``RunResult``, ``run_ftrl``, ``replay_exact_ftl``,
 ``simulate`` and ``run_ftl_exact``; the FTRL loop (exact_ftl.py:230-277) and the
 replay (:306-333) run in the HIP kernels.
 
-Out of scope this round: the cvxpy SOCP comparator
-``ExactFTLNoClip`` (exact_ftl.py:62-193) — cvxpy is not available, so there is no
-reference oracle for it (parity unpinned).  Calls that would need it raise
-``NotImplementedError``; a caller-supplied ``comparator_action`` /
-``prefix_actions`` (or any ``comparator_solver`` object with the reference's
-``solve_prefix_from_full`` method) works.
+The exact FTL solutions (the cvxpy SOCP of ``ExactFTLNoClip``, exact_ftl.py:62-193)
+are computed on the GPU in closed form for the l2 ball whenever the data satisfy
+||z_t|| <= 1 and y_t = ±1 — every sequence family and adversary of the reference does:
+there ½Σ|z_i·x − y_i| is linear on the ball and its minimiser is S_t/||S_t||,
+S_t = Σ_{i<t} y_i z_i (engine.ftl_exact_batch).  Outside that regime, and for the l1 /
+linf balls, the general SOCP is out of scope: cvxpy is absent, so its results are
+unpinned and those calls raise ``NotImplementedError`` unless the caller
+supplies ``comparator_action`` / ``prefix_actions`` or a solver object with the
+reference's methods.
 """
 from __future__ import annotations
 
@@ -19,8 +22,9 @@ from typing import Literal, Optional, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import ptr
+from . import engine as _engine
 from . import fast_algorithms as _fa
+from ._lib import ptr
 
 
 @dataclass
@@ -55,10 +59,12 @@ def _simulate_ftrl(z_arr, y_arr, *, eta0, comparator_action=None, comparator_sol
     """exact_ftl.py:230-277 on the GPU."""
     T, d = z_arr.shape
     if comparator_action is None:
-        if comparator_solver is None:
-            raise NotImplementedError("the exact SOCP comparator needs cvxpy (out of scope); "
-                                      "pass comparator_action")
-        comparator_action = comparator_solver.solve_prefix_from_full(z_arr, y_arr, T)
+        if comparator_solver is not None:
+            comparator_action = comparator_solver.solve_prefix_from_full(z_arr, y_arr, T)
+        else:  # exact SOCP solution of the whole sequence, closed form on the GPU
+            _, _, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
+                                                   device=_fa._DEVICE)
+            comparator_action = act[0]
     comp_vec = _ensure_float64_contiguous(comparator_action)
     if comp_vec.shape != (d,):
         raise ValueError(f"comparator_action must have shape ({d},)")
@@ -100,6 +106,14 @@ def _prefix_actions_from_solver(ftl_solver, z_arr, y_arr) -> np.ndarray:
     return actions
 
 
+def _ftl_exact_gpu(z_arr, y_arr, norm) -> RunResult:
+    """exact_ftl.py:423-453 with the prefix actions solved on the GPU (closed form)."""
+    cum, comp, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
+                                                device=_fa._DEVICE)
+    return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - comp[0]),
+                     comp_loss=float(comp[0]), x_last=act[0].copy())
+
+
 def simulate(z, y, *, algo: Literal["ftrl", "ftl_exact"] = "ftl_exact", eta0: float = 1.0,
              norm: Literal["l2", "linf", "l1"] = "l2", solver: Optional[str] = None,
              solver_opts: Optional[dict] = None, ftl_solver=None, comparator_solver=None,
@@ -109,10 +123,9 @@ def simulate(z, y, *, algo: Literal["ftrl", "ftl_exact"] = "ftl_exact", eta0: fl
     z_arr = _ensure_float64_contiguous(z)
     y_arr = _ensure_float64_contiguous(y)
     if algo == "ftl_exact":
+        if prefix_actions is None and ftl_solver is None:
+            return _ftl_exact_gpu(z_arr, y_arr, norm)
         if prefix_actions is None:
-            if ftl_solver is None:
-                raise NotImplementedError("exact FTL prefix actions need the cvxpy solver "
-                                          "(out of scope); pass prefix_actions")
             prefix_actions = _prefix_actions_from_solver(ftl_solver, z_arr, y_arr)
         return replay_exact_ftl(z_arr, y_arr, prefix_actions)
     if algo == "ftrl":
@@ -134,14 +147,18 @@ def run_ftrl(z, y, *, eta0: float = 1.0, norm: Literal["l2", "linf", "l1"] = "l2
 def run_ftl_exact(z, y, *, norm="l2", solver=None, solver_opts=None, ftl_solver=None,
                   prefix_actions: Optional[np.ndarray] = None, return_actions: bool = False
                   ) -> RunResult | Tuple[RunResult, np.ndarray]:
-    """exact_ftl.py:423-453 (needs ``prefix_actions`` or a caller-supplied ``ftl_solver``)."""
+    """exact_ftl.py:423-453.  Without ``prefix_actions`` or ``ftl_solver`` the prefix
+    actions are solved on the GPU (closed form, l2 ball) and replayed in the same kernel;
+    the T+1 actions are not materialised, so ``return_actions=True`` needs one of the two."""
     z_arr = _ensure_float64_contiguous(z)
     y_arr = _ensure_float64_contiguous(y)
     actions = prefix_actions
+    if actions is None and ftl_solver is None and not return_actions:
+        return _ftl_exact_gpu(z_arr, y_arr, norm)
     if actions is None:
         if ftl_solver is None:
-            raise NotImplementedError("exact FTL prefix actions need the cvxpy solver "
-                                      "(out of scope); pass prefix_actions")
+            raise NotImplementedError("return_actions=True needs prefix_actions or a solver "
+                                      "object (the GPU path does not materialise T+1 actions)")
         actions = _prefix_actions_from_solver(ftl_solver, z_arr, y_arr)
     result = replay_exact_ftl(z_arr, y_arr, actions)
     if return_actions:

@@ -160,6 +160,38 @@ int oc_simulate_smart(const double *z, const double *y, int64_t T, int64_t d, do
     return 0;
 }
 
+/* exact_ftl.py:280-333 (compute_prefix_actions + replay_exact_ftl, l2 ball) in closed
+ * form.  When every ||z_t|| <= 1 and y_t = +-1 the objective 0.5*sum|z_i.x - y_i| equals
+ * 0.5*(t - x.S_t) on the unit ball, so the prefix minimiser is S_t/||S_t|| (0 if S_t = 0),
+ * S_t = sum_{i<t} y_i z_i: the FTL action (fast_algorithms.py:37-49) of theta = -S_t.
+ * The reference obtains the same points from cvxpy (absent here; parity unpinned): this
+ * restatement is checked against an independent scipy solver in tests/. */
+int oc_ftl_exact(const double *z, const double *y, int64_t T, int64_t d, double *cum_out,
+                 double *comp_out, double *cmp_action, int *regime) {
+    double *theta = (double *)calloc((size_t)(d > 0 ? d : 1), sizeof(double));
+    double *x = (double *)calloc((size_t)(d > 0 ? d : 1), sizeof(double));
+    if (!theta || !x) { free(theta); free(x); return -1; }
+    int linear = 1;
+    double cum = 0.0;
+    for (int64_t t = 0; t < T; ++t) {
+        const double *zt = z + t * d;
+        oc_action_ftl(theta, d, x);
+        cum += oc_normalized_hinge(oc_dot(zt, x, d), y[t]);
+        double zz = 0.0;
+        for (int64_t j = 0; j < d; ++j) zz += zt[j] * zt[j];
+        if (!(zz <= 1.0 + 1e-6 && fabs(y[t]) == 1.0)) linear = 0;
+        for (int64_t j = 0; j < d; ++j) theta[j] += (-y[t]) * zt[j];
+    }
+    oc_action_ftl(theta, d, x);
+    double comp = oc_comparator_loss_prefix(z, y, d, x, T);
+    if (cum_out) *cum_out = cum;
+    if (comp_out) *comp_out = comp;
+    if (cmp_action) memcpy(cmp_action, x, (size_t)d * sizeof(double));
+    if (regime) *regime = linear;
+    free(theta); free(x);
+    return 0;
+}
+
 /* exact_ftl.py:306-333 `replay_exact_ftl` loop: actions is [T+1][d]. */
 int oc_replay(const double *z, const double *y, int64_t T, int64_t d, const double *actions,
               double *cum_loss_out) {

@@ -65,6 +65,8 @@ def lib():
                                               ctypes.c_int64, _dp, ctypes.c_double, _dp, _i64p,
                                               ctypes.c_int]
         L.oc_max_threads.restype = ctypes.c_int
+        L.oc_ftl_exact.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp, _dp,
+                                   ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -133,6 +135,20 @@ def replay_cum_loss(z, y, actions) -> float:
     out = np.zeros(1, dtype=np.float64)
     lib().oc_replay(_ptr(z), _ptr(y), T, d, _ptr(a), _ptr(out))
     return float(out[0])
+
+
+def ftl_exact_closed_form(z, y):
+    """exact_ftl.py:280-333 (l2 ball) in closed form → (cum_loss, comp_loss, actions[T],
+    in_regime).  See oc_ftl_exact in ocx_oracle.c."""
+    z = _f64(z)
+    y = _f64(y)
+    T, d = z.shape
+    out = np.zeros(2)
+    a = np.zeros(d)
+    rg = ctypes.c_int(0)
+    lib().oc_ftl_exact(_ptr(z), _ptr(y), T, d, _ptr(out[0:1]), _ptr(out[1:2]), _ptr(a),
+                       ctypes.byref(rg))
+    return float(out[0]), float(out[1]), a, bool(rg.value)
 
 
 def comparator_loss_blas(z, y, x) -> float:

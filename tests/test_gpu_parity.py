@@ -320,3 +320,53 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
             assert close(chunked[r], ref)
         else:
             assert chunked[r] == ref
+
+
+# ------------------------------------------------------------------ exact FTL (closed form)
+def test_ftl_exact_matches_oracle(ocx):
+    """exact_ftl run_ftl_exact / run_ftrl(no comparator) on the GPU == the oracle's closed
+    form (the closed form itself is checked against scipy in test_exact_comparator_cpu)."""
+    eng, ef = ocx["engine"], ocx["ef"]
+    rng = np.random.default_rng(11)
+    B, T, d = 21, 300, 7
+    z = rng.standard_normal((B, T, d))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    for P in (1, -1, 4):
+        cum, comp, act, ok = eng.ftl_exact_batch(z, y, lanes_per_seq=P)
+        assert ok.all()
+        for b in range(B):
+            rc, rp, ra, rin = O.ftl_exact_closed_form(z[b], y[b])
+            if P != 4:
+                assert (cum[b], comp[b]) == (rc, rp) and np.array_equal(act[b], ra), (P, b)
+            else:
+                assert close([cum[b], comp[b]], [rc, rp]) and close(act[b], ra)
+    res = ef.run_ftl_exact(z[0], y[0])
+    rc, rp, ra, _ = O.ftl_exact_closed_form(z[0], y[0])
+    assert (res.cum_loss, res.comp_loss) == (rc, rp) and np.array_equal(res.x_last, ra)
+    rr = ef.run_ftrl(z[1], y[1], eta0=SQ2)
+    _, _, a1, _ = O.ftl_exact_closed_form(z[1], y[1])
+    ref = O.simulate_alg_full(z[1], y[1], 0, SQ2, comparator=a1)
+    assert (rr.regret, rr.cum_loss, rr.comp_loss) == ref[:3]
+    with pytest.raises(NotImplementedError):
+        ef.run_ftl_exact(2.0 * z[0], y[0])
+
+
+def test_exact_driver_matches_oracle(ocx):
+    from online_convex_optimization_amd import drivers
+    runs, reps, T = 2, 3, 120
+    st = drivers.exact_evaluate_stream_with_stats("Random i.i.d. (separable)", [T], runs=runs,
+                                                  replicates=reps)
+    ftrl, ftl = [], []
+    for r in range(runs):
+        fr, fl = [], []
+        for rep in range(reps):
+            z, y, _ = O.random_iid_sample(2025 * (r + 1), T, rep)
+            c, p, a, ok = O.ftl_exact_closed_form(z, y)
+            assert ok
+            fl.append(c - p)
+            fr.append(O.simulate_alg_full(z, y, 0, SQ2, comparator=a)[0])
+        ftrl.append(float(np.mean(fr)))
+        ftl.append(float(np.mean(fl)))
+    assert st["FTRL"][0][0] == float(np.mean(ftrl))
+    assert st["FTL (exact)"][0][0] == float(np.mean(ftl))
