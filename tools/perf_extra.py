@@ -68,6 +68,46 @@ def driver(args):
     print(json.dumps(out), flush=True)
 
 
+def config3(args):
+    """configs[2]: exact_ftl vs fast FTRL, d=64, T=1e4, 1e5 trials on one GPU: per trial
+    FTRL's regret against the exact comparator and against its own FTL comparator,
+    generation included (resident batches of 32768)."""
+    import torch
+    from online_convex_optimization_amd import engine
+    T, d, trials, Bb = 10000, 64, 100000, 32768
+    t0 = time.perf_counter()
+    diffs = []
+    for r0 in range(0, trials, Bb):
+        B = min(Bb, trials - r0)
+        db = engine.DeviceBatch(B, T, d, lanes_per_seq=1)
+        db.generate_gT(0, r0)
+        act = torch.zeros((B, d), dtype=torch.float64, device=db.device)
+        regime = db.ftl_exact(cmp_action=act)
+        exact = db.simulate_alg(0, math.sqrt(2), comparator=act).clone()
+        fast = db.simulate_alg(0, math.sqrt(2)).clone()
+        assert bool(regime[:B].all())
+        diffs.append((exact[:B] - fast[:B]).cpu().numpy())
+        del db
+    sync()
+    dt = time.perf_counter() - t0
+    dd = np.concatenate(diffs)
+    print(json.dumps({"what": "config3_exact_vs_fast", "trials": trials, "T": T, "d": d,
+                      "seconds": dt, "trial_steps_per_s": trials * T / dt,
+                      "mean_regret_exact_minus_fast": float(dd.mean()),
+                      "max_abs_diff": float(np.abs(dd).max())}), flush=True)
+
+
+def exact_driver(args):
+    from online_convex_optimization_amd import drivers
+    t0 = time.perf_counter()
+    g, stats = drivers.exact_ftl_driver_main()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"what": "exact_ftl_driver_main", "seconds": dt,
+                      "g_emp": [g[T] for T in range(100, 1100, 100)],
+                      "T1000": {t: {k: float(v[0][-1]) for k, v in st.items()}
+                                for t, st in stats.items()}}), flush=True)
+
+
 def smart(args):
     from online_convex_optimization_amd import engine
     import torch
@@ -87,7 +127,7 @@ def smart(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["gen", "sweep", "driver", "smart"])
+    ap.add_argument("what", nargs="+", choices=["gen", "sweep", "driver", "smart", "config3", "exact_driver"])
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
