@@ -22,7 +22,7 @@ BUILD = os.path.join(ROOT, "build", "ocx")
 LIB = os.path.join(PKG, "libocx.so")
 ARCH = os.environ.get("OCX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["ocx_sim.hip", "ocx_gen.hip", "ocx_stream.hip", "ocx_capi.hip"]
+SOURCES = ["ocx_sim.hip", "ocx_gen.hip", "ocx_gen_wave.hip", "ocx_stream.hip", "ocx_capi.hip"]
 HEADERS = ["ocx_internal.h", "ocx_rng.h", "ocx_sim_kernels.h", "zig_tables.h",
            "ocx_device_math.h", "ocx_dispatch.h"]
 
@@ -73,20 +73,21 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
     return LIB
 
 
-def build_variant(name: str, defines, jobs: int = 4) -> str:
-    """Tuning variant: ocx_sim.hip recompiled with -D overrides, linked into
-    tune_build/libocx_<name>.so (never loaded by the product path)."""
+def build_variant(name: str, defines, jobs: int = 4, source: str = "ocx_sim.hip") -> str:
+    """Tuning variant: one source recompiled with -D overrides, linked with the other
+    objects into tune_build/libocx_<name>.so (never loaded by the product path; select it
+    with OCX_LIB)."""
     hipcc = _hipcc()
     out_dir = os.path.join(ROOT, "tune_build")
     os.makedirs(out_dir, exist_ok=True)
     build(jobs=jobs)  # the shared objects of the other sources
-    obj = os.path.join(out_dir, f"ocx_sim_{name}.o")
+    obj = os.path.join(out_dir, f"{source.replace('.hip', '')}_{name}.o")
     lib = os.path.join(out_dir, f"libocx_{name}.so")
     dflags = [f"-D{d}" for d in defines]
-    src = os.path.join(CSRC, "ocx_sim.hip")
+    src = os.path.join(CSRC, source)
     if _stale(lib, [src, *[os.path.join(CSRC, h) for h in HEADERS]]):
         subprocess.run([hipcc, *CFLAGS, *dflags, "-c", src, "-o", obj], check=True)
-        others = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES if s != "ocx_sim.hip"]
+        others = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES if s != source]
         subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", obj, *others, "-o", lib],
                        check=True)
     return lib

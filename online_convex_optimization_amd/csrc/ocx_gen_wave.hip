@@ -1,0 +1,557 @@
+// ocx_gen_wave.hip — the g(T) adversary (fast_algorithms.py:231-239) with one
+// wavefront per NumPy stream.
+//
+// NumPy's ziggurat is sequential per stream, but 99.3 % of its draws are accepted on
+// the fast path, so a wave speculates: lane k computes raw draw k of the stream by
+// PCG64 jump-ahead (state_{n+k+1} = A^{k+1} state_n + inc·(A^k + … + 1)), runs the
+// fast test, and the wave then parses the 64 draws in stream order.  A rejected draw
+// k consumes draw k+1 as its wedge uniform (a lane-parallel test; exp() is only
+// evaluated exactly when a float estimate is too close to call), a tail draw falls
+// back to NumPy's sequential loop, and the accepted normals are appended to a
+// per-wave LDS ring with mbcnt.  Whole rows leave the ring: their sum of squares in
+// NumPy's pairwise order (8 strided accumulators, combined by the DPP butterfly
+// of ocx_seq_sum<8>, which reproduces ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) bit for
+// bit), the clip scale 1/max(‖z_t‖, 1), and a store into the tiled layout.  The
+// ±1 labels (choice → top bit of each buffered uint32) follow, 128 per round.
+//
+// Compared with one lane per stream (ocx_gen.hip's row staging, 33 KB of LDS per
+// wave): no per-lane rows, so occupancy is set by registers, every lane works on
+// every round, and a batch of a few thousand sequences already fills the GPU.
+#include <algorithm>
+
+#include "ocx_internal.h"
+#include "ocx_rng.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
+
+struct ZigTables {
+    uint64_t ki[256];
+    double wi[256];
+    double fi[256];
+};
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), lane) << 32) | rl32((uint32_t)v, lane);
+}
+__device__ __forceinline__ ocx_u128 rl128(ocx_u128 v, int lane) {
+    return ((ocx_u128)rl64((uint64_t)(v >> 64), lane) << 64) | rl64((uint64_t)v, lane);
+}
+__device__ __forceinline__ uint64_t shfl_down1(uint64_t v) {
+    const int addr = (int)(((threadIdx.x & 63) + 1) & 63) << 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ double shfl_double(double v, int src) {
+    const int addr = src << 2;
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint64_t lowmask(int n) {
+    return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL);
+}
+__device__ __forceinline__ uint64_t xsl_rr(ocx_u128 s) {
+    const uint64_t hi = (uint64_t)(s >> 64), lo = (uint64_t)s;
+    const unsigned rot = (unsigned)(hi >> 58);
+    const uint64_t x = hi ^ lo;
+    return (x >> rot) | (x << ((0u - rot) & 63u));
+}
+__device__ __forceinline__ double u53(uint64_t r) {
+    return (double)(r >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Rare paths, kept out of line so their constants do not occupy registers of the
+// round loop: the exact wedge comparison (float estimate too close to call, ~1e-5 of
+// wedge tests) and NumPy's tail loop (≈3e-4 of draws).
+__device__ __noinline__ bool wedge_exact(double lhs, double a) { return lhs < exp(a); }
+
+struct TailOut {
+    double v;
+    uint64_t lo, hi;
+};
+
+__device__ __noinline__ TailOut zig_tail(uint64_t st_lo, uint64_t st_hi, uint64_t inc_lo,
+                                        uint64_t inc_hi, uint64_t rabs) {
+    ocx_pcg64 g;
+    g.state = ((ocx_u128)st_hi << 64) | st_lo;
+    g.inc = ((ocx_u128)inc_hi << 64) | inc_lo;
+    g.buf32 = 0;
+    g.has32 = 0;
+    double xx, yy;
+    for (;;) {
+        xx = -OCX_ZIG_NOR_INV_R * ocx_log1p(-ocx_pcg_next_double(&g));
+        yy = -ocx_log1p(-ocx_pcg_next_double(&g));
+        if (yy + yy > xx * xx) break;
+    }
+    TailOut o;
+    o.v = ((rabs >> 8) & 0x1) ? -(OCX_ZIG_NOR_R + xx) : OCX_ZIG_NOR_R + xx;
+    o.lo = (uint64_t)g.state;
+    o.hi = (uint64_t)(g.state >> 64);
+    return o;
+}
+
+// One stream, as a wave sees it: the uniform state and increment, and this lane's
+// jump-ahead pair (state after draw k of a round = Ak * base + Dk).
+struct WaveStream {
+    ocx_u128 base, inc;
+    ocx_u128 Ak, Dk;
+};
+
+__device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u128 Gk) {
+    w.base = g.state;
+    w.inc = g.inc;
+    w.Dk = g.inc * Gk;
+}
+
+// One round: speculate 64 draws, parse them in stream order, append at most `need`
+// normals to the ring at `head` (when RING).  Returns the number appended and advances
+// the stream past exactly the draws those normals consumed (NumPy random_standard_normal).
+template <bool RING>
+__device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
+                         unsigned head, int lane) {
+    const ocx_u128 s = w.Ak * w.base + w.Dk;
+    const uint64_t r = xsl_rr(s);
+    const int idx = (int)(r & 0xff);
+    const uint64_t r8 = r >> 8;
+    const uint64_t rabs = (r8 >> 1) & kMask52;
+    double x = (double)rabs * tb.wi[idx];
+    if (r8 & 1) x = -x;
+    const bool fast = rabs < tb.ki[idx];
+    const uint64_t rej = ballot(!fast);
+    if (rej == 0 && need == 64) {  // every draw accepted (64 % of rounds)
+        if (RING) ring[(head + (unsigned)lane) & rmask] = x;
+        w.base = rl128(s, 63);
+        return 64;
+    }
+    uint64_t cons = 0, wacc = 0;
+    int limit = 64, tail_k = -1;
+    if (rej) {
+        // wedge test of a rejected draw k uses draw k+1 (next_double) as its uniform
+        const uint64_t rn = shfl_down1(r);
+        bool wa = false;
+        if (!fast && idx != 0) {
+            const double lhs = (tb.fi[idx - 1] - tb.fi[idx]) * u53(rn) + tb.fi[idx];
+            const double a = -0.5 * x * x;
+            const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
+            if (lhs < e * (1.0 - 1e-5)) wa = true;
+            else if (lhs > e * (1.0 + 1e-5)) wa = false;
+            else wa = wedge_exact(lhs, a);
+        }
+        wacc = ballot(wa);
+        const uint64_t tailm = ballot(!fast && idx == 0);
+        uint64_t rem = rej;
+        while (rem) {
+            const int k = __builtin_ctzll(rem);
+            rem &= rem - 1;
+            if ((cons >> k) & 1) continue;  // this draw is an earlier wedge's uniform
+            if ((tailm >> k) & 1) {
+                limit = k;
+                tail_k = k;
+                break;
+            }
+            if (k == 63) {  // its uniform is not in this round: redo it next round
+                limit = 63;
+                break;
+            }
+            cons |= 1ULL << (k + 1);
+        }
+    }
+    uint64_t emit = (~rej | (rej & wacc)) & ~cons & lowmask(limit);
+    int n = __builtin_popcountll(emit);
+    int m = limit;  // draws consumed
+    if (n >= need) {
+        int p;  // lane of the need-th normal
+        if (n == need) {
+            p = 63 - __builtin_clzll(emit);
+        } else {  // only in the last round of a sequence or chunk
+            uint64_t e = emit;
+            for (int i = 1; i < need; ++i) e &= e - 1;
+            p = __builtin_ctzll(e);
+        }
+        emit &= lowmask(p + 1);
+        m = ((rej >> p) & 1) ? p + 2 : p + 1;
+        n = need;
+        tail_k = -1;
+    }
+    if (RING && ((emit >> lane) & 1)) ring[(head + mbcnt(emit)) & rmask] = x;
+    if (tail_k >= 0) {
+        // NumPy's tail loop, sequential from the state after the tail draw
+        const ocx_u128 st = rl128(s, tail_k);
+        const TailOut o = zig_tail((uint64_t)st, (uint64_t)(st >> 64), (uint64_t)w.inc,
+                                   (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
+        if (RING && lane == 0) ring[(head + n) & rmask] = o.v;
+        w.base = ((ocx_u128)o.hi << 64) | o.lo;
+        return n + 1;
+    }
+    w.base = rl128(s, m - 1);
+    return n;
+}
+
+// NumPy pairwise sum of v*v over one leaf of n <= 128 ring values starting at o.
+__device__ __forceinline__ double leaf_sumsq(const double* ring, int rmask, unsigned o, int n,
+                                             int lane) {
+    double res = 0.0;
+    int i = 0;
+    if (n >= 8) {
+        const int n8 = n - (n % 8);
+        const int k = lane & 7;
+        double v = ring[(o + k) & rmask];
+        double acc = v * v;
+        for (int j = k + 8; j < n8; j += 8) {
+            v = ring[(o + j) & rmask];
+            acc += v * v;
+        }
+        res = ocx_seq_sum<8>(acc);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) in every lane
+        i = n8;
+    }
+    for (; i < n; ++i) {
+        const double v = ring[(o + i) & rmask];
+        res += v * v;
+    }
+    return res;
+}
+
+// np.linalg.norm(z, axis=1)**2 for one row of d values (pairwise_sum recursion above
+// 128 elements: split at n/2 rounded down to a multiple of 8, left + right).  The
+// post-order walk of that recursion keeps its (uniform) stack in the wave's LDS slot
+// `stk` so no register array is indexed dynamically.
+struct PwFrame {
+    unsigned o;
+    int n, state;
+    double val;
+};
+
+__device__ double row_sumsq(const double* ring, int rmask, unsigned o, int d, int lane,
+                            PwFrame* stk) {
+    if (d <= 128) return leaf_sumsq(ring, rmask, o, d, lane);
+    int sp = 0;
+    if (lane == 0) stk[0] = PwFrame{o, d, 0, 0.0};
+    double ret = 0.0;
+    for (;;) {
+        __builtin_amdgcn_wave_barrier();
+        const PwFrame f = stk[sp];
+        if (f.n <= 128) {
+            ret = leaf_sumsq(ring, rmask, f.o, f.n, lane);
+        } else if (f.state < 2) {
+            int n2 = f.n / 2;
+            n2 -= n2 % 8;
+            if (lane == 0) {
+                stk[sp].state = f.state + 1;
+                if (f.state == 1) stk[sp].val = ret;
+                stk[sp + 1] = (f.state == 0) ? PwFrame{f.o, n2, 0, 0.0}
+                                             : PwFrame{f.o + (unsigned)n2, f.n - n2, 0, 0.0};
+            }
+            ++sp;
+            continue;
+        } else {
+            ret = f.val + ret;
+        }
+        if (sp == 0) return ret;
+        --sp;
+    }
+}
+
+__device__ __forceinline__ void save_state6(uint64_t* p, ocx_u128 state, ocx_u128 inc,
+                                            uint32_t buf32, int has32) {
+    p[0] = (uint64_t)state;
+    p[1] = (uint64_t)(state >> 64);
+    p[2] = (uint64_t)inc;
+    p[3] = (uint64_t)(inc >> 64);
+    p[4] = (uint64_t)buf32 | ((uint64_t)(uint32_t)has32 << 32);
+    p[5] = 0;
+}
+
+__device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, ocx_u128& inc,
+                                            uint32_t& buf32, int& has32) {
+    state = ((ocx_u128)p[1] << 64) | p[0];
+    inc = ((ocx_u128)p[3] << 64) | p[2];
+    buf32 = (uint32_t)p[4];
+    has32 = (int)(p[4] >> 32);
+}
+
+constexpr int kWaveBlock = 256;
+#ifndef OCX_GENW_MIN_WAVES
+#define OCX_GENW_MIN_WAVES 1  // waves per SIMD the register allocation must allow
+#endif
+
+// rows per batch leaving the ring (see the kernel)
+__host__ __device__ __forceinline__ int batch_rows(int d) {
+    if (d < 8) return 32;
+    if (d <= 128) return d <= 32 ? 8 : (d <= 64 ? 4 : 2);
+    return 1;
+}
+constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion depth <= 16
+
+}  // namespace
+
+// MODE 0 (generate): rows [0, T) of the tiled layout (z_t clipped, fast_algorithms.py:
+//   234-237) and then the labels (:239).  Fresh streams _rng(base_seed, T_seed, run0+b),
+//   or, in chunk mode (st_in != nullptr), rows resume from st_in[b] (saved to st_out[b])
+//   and labels from lab_in[b] (saved to lab_out[b]).
+// MODE 1 (seek): st_out[b] = the fresh stream, lab_out[b] = the stream after its
+//   T_seed·d normals, i.e. where choice(T) starts.
+template <int MODE>
+__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_kernel(
+    uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
+    int d, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
+    const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
+    const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out, int rb,
+    int64_t nwaves) {
+    __shared__ ZigTables tb;
+    extern __shared__ double rings[];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        tb.ki[i] = OCX_ZIG_KI[i];
+        tb.wi[i] = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
+        tb.fi[i] = __longlong_as_double((long long)OCX_ZIG_FI_BITS[i]);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6);
+    if (wave >= nwaves) return;
+    double* ring = rings + (threadIdx.x >> 6) * (rb + kStackDoubles);
+    PwFrame* stk = reinterpret_cast<PwFrame*>(ring + rb);
+    const int rmask = rb - 1;
+
+    // jump-ahead constants of this lane: A^(k+1) and A^k + ... + A + 1
+    WaveStream w;
+    ocx_u128 Gk = 0;
+    {
+        ocx_u128 a = 1;
+        for (int i = 0; i <= lane; ++i) {
+            Gk = Gk * OCX_PCG_MULT + 1;
+            a = a * OCX_PCG_MULT;
+        }
+        w.Ak = a;
+    }
+    const int S = 64 / P;
+    const int Dp = P * C;
+    // rows leave the ring in batches of R: the sums of squares of a batch run side by
+    // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
+    const int R = batch_rows(d);
+    // store map for Dp <= 64: lane → (row of the pass, coordinate j), RP rows per pass
+    const int RP = Dp <= 64 ? 64 / Dp : 1;
+    const int jl = Dp <= 64 ? lane % Dp : lane;
+    const int rl = Dp <= 64 ? lane / Dp : 0;
+    const int cl = jl / C, kl = (jl - cl * C) >> 1, el = (jl - cl * C) & 1;
+
+    for (int64_t b = wave; b < nseq; b += nwaves) {
+        const int64_t g = b / S;
+        const int s = (int)(b - g * S);
+        double* yrow = ytl + g * T * S + s;
+        // tile offset of (t = 0, j = jl) for this sequence (Dp <= 64)
+        const int64_t zoff = ((int64_t)kl * G + g) * T * 128 + (s * P + cl) * 2 + el;
+        auto zaddr = [&](int64_t t, int j) -> double* {  // general j (Dp > 64)
+            const int c = j / C, rr = j - c * C;
+            return zt + (((int64_t)(rr >> 1) * G + g) * T + t) * 128 + (s * P + c) * 2 + (rr & 1);
+        };
+        if (MODE == 0 && (b >= B || d == 0)) {  // padding sequence / empty rows: zeros
+            for (int64_t t = 0; t < T; ++t)
+                for (int j = lane; j < Dp; j += 64) *zaddr(t, j) = 0.0;
+            if (b >= B) {
+                for (int64_t t = lane; t < T; t += 64) yrow[t * S] = 0.0;
+                continue;
+            }
+        }
+        ocx_pcg64 g0;
+        if (MODE == 0 && st_in != nullptr) {
+            load_state6(st_in + 6 * b, g0.state, g0.inc, g0.buf32, g0.has32);
+        } else {
+            ocx_rng_init3(&g0, base_seed, (uint64_t)T_seed, (uint64_t)(run0 + b));
+            if (MODE == 1 && lane == 0) save_state6(st_out + 6 * b, g0.state, g0.inc, 0, 0);
+        }
+        ws_set(w, g0, Gk);
+
+        // ---- rows
+        const int64_t rows = (MODE == 0) ? T : T_seed;
+        int64_t remaining = rows * d;  // normals still to draw
+        unsigned head = 0, tailp = 0;  // ring counters (mod 2^32; masked on use)
+        unsigned partial = 0;          // normals of the row being filled
+        int ready = 0;                 // whole rows waiting in the ring
+        int64_t t = 0;
+        while (remaining > 0) {
+            const int need = remaining < 64 ? (int)remaining : 64;
+            const int n = zig_round<MODE == 0>(w, need, tb, ring, rmask, head, lane);
+            head += n;
+            remaining -= n;
+            if (MODE != 0) continue;
+            partial += (unsigned)n;
+            while (partial >= (unsigned)d) {
+                partial -= (unsigned)d;
+                ++ready;
+            }
+            while (ready >= R || (remaining == 0 && ready > 0)) {
+                const int nrows = ready < R ? ready : R;
+                // this lane's row of the batch and its clip scale
+                double sc = 1.0;
+                if (d <= 128) {
+                    const int r = d < 8 ? lane : (lane >> 3);
+                    const unsigned o = tailp + (unsigned)(r * d);
+                    double ss = 0.0;
+                    if (d < 8) {
+                        for (int i = 0; i < d; ++i) {
+                            const double v = ring[(o + i) & rmask];
+                            ss += v * v;
+                        }
+                    } else {
+                        ss = leaf_sumsq(ring, rmask, o, d, lane);
+                    }
+                    const double nrm = sqrt(ss);
+                    sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
+                }
+                const int sc_stride = d < 8 ? 1 : 8;
+                if (Dp <= 64 && d <= 128 && RP == 1) {
+                    for (int r = 0; r < nrows; ++r) {
+                        const double scr = __hiloint2double(
+                            __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
+                            __builtin_amdgcn_readlane(__double2loint(sc), r * sc_stride));
+                        if (rl == 0) {
+                            const double v =
+                                jl < d ? ring[(tailp + (unsigned)(r * d + jl)) & rmask] * scr : 0.0;
+                            __builtin_nontemporal_store(v, zt + zoff + (t + r) * 128);
+                        }
+                    }
+                } else if (Dp <= 64 && d <= 128) {
+                    for (int r0 = 0; r0 < nrows; r0 += RP) {
+                        const int r = r0 + rl;
+                        const double scr = shfl_double(sc, (r < 64 / sc_stride ? r : 0) * sc_stride);
+                        if (rl < RP && r < nrows) {
+                            const double v =
+                                jl < d ? ring[(tailp + (unsigned)(r * d + jl)) & rmask] * scr : 0.0;
+                            __builtin_nontemporal_store(v, zt + zoff + (t + r) * 128);
+                        }
+                    }
+                } else {
+                    for (int r = 0; r < nrows; ++r) {
+                        const unsigned o = tailp + (unsigned)(r * d);
+                        double scr;
+                        if (d > 128) {
+                            const double nrm = sqrt(row_sumsq(ring, rmask, o, d, lane, stk));
+                            scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
+                        } else {
+                            scr = shfl_double(sc, r * sc_stride);
+                        }
+                        for (int j = lane; j < Dp; j += 64) {
+                            const double v = j < d ? ring[(o + (unsigned)j) & rmask] * scr : 0.0;
+                            __builtin_nontemporal_store(v, zaddr(t + r, j));
+                        }
+                    }
+                }
+                tailp += (unsigned)(nrows * d);
+                t += nrows;
+                ready -= nrows;
+            }
+        }
+        if (MODE == 1) {
+            if (lane == 0) save_state6(lab_out + 6 * b, w.base, w.inc, 0, 0);
+            continue;
+        }
+        if (st_in != nullptr && st_out != nullptr && lane == 0)
+            save_state6(st_out + 6 * b, w.base, w.inc, 0, 0);
+
+        // ---- labels: choice([-1., 1.], T) = top bit of each buffered uint32, low half first
+        uint32_t buf32 = 0;
+        int has32 = 0;
+        if (lab_in != nullptr) {
+            ocx_u128 ls, li;
+            load_state6(lab_in + 6 * b, ls, li, buf32, has32);
+            w.base = ls;
+        }
+        int64_t tl = 0;
+        if (has32 && T > 0) {
+            if (lane == 0) yrow[0] = (buf32 >> 31) ? 1.0 : -1.0;
+            has32 = 0;
+            tl = 1;
+        }
+        while (tl < T) {
+            const int64_t left = T - tl;
+            const int ndraw = left >= 128 ? 64 : (int)((left + 1) / 2);
+            const ocx_u128 st = w.Ak * w.base + w.Dk;
+            const uint64_t r = xsl_rr(st);
+            const int64_t t0 = tl + 2 * lane;
+            if (lane < ndraw) {
+                yrow[t0 * S] = (((uint32_t)r) >> 31) ? 1.0 : -1.0;
+                if (t0 + 1 < T) yrow[(t0 + 1) * S] = (((uint32_t)(r >> 32)) >> 31) ? 1.0 : -1.0;
+            }
+            if (left < 128 && (left & 1)) {  // the last draw's high half stays buffered
+                has32 = 1;
+                buf32 = (uint32_t)(rl64(r, ndraw - 1) >> 32);
+            }
+            w.base = rl128(st, ndraw - 1);
+            tl += 2 * (int64_t)ndraw;
+        }
+        if (lab_out != nullptr && lane == 0) save_state6(lab_out + 6 * b, w.base, w.inc, buf32, has32);
+    }
+}
+
+namespace {
+
+int ring_doubles(int64_t d) {
+    // a full batch of rows plus one round of normals
+    int rb = 128;
+    while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
+    return rb;
+}
+
+template <int MODE>
+hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq,
+                       int64_t T, int64_t d, int P, int C, int64_t G, double* zt, double* ytl,
+                       const uint64_t* st_in, uint64_t* st_out, const uint64_t* lab_in,
+                       uint64_t* lab_out, hipStream_t st) {
+    const int rb = (MODE == 0) ? ring_doubles(d) : 0;
+    const size_t lds = (MODE == 0) ? (size_t)(rb + kStackDoubles) * 8 * (kWaveBlock / 64) : 0;
+    // resident waves: fill the GPU once, sequences spread evenly over the waves
+    int dev = 0, cus = 256, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE>,
+                                                     kWaveBlock, lds);
+    if (e != hipSuccess) return e;
+    const int64_t resident = std::max<int64_t>(1, (int64_t)cus * std::max(per_cu, 1) * (kWaveBlock / 64));
+    const int64_t per_wave = (nseq + resident - 1) / resident;
+    const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
+    const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));
+    hipLaunchKernelGGL(ocx_gen_wave_kernel<MODE>, dim3(blocks), dim3(kWaveBlock), lds, st,
+                       base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
+                       st_out, lab_in, lab_out, rb, nwaves);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
+                             double* ytl, hipStream_t st) {
+    const int64_t nseq = L->G * L->S;
+    if (nseq == 0 || L->T == 0) return hipSuccess;
+    return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt,
+                          ytl, nullptr, nullptr, nullptr, nullptr, st);
+}
+
+hipError_t ocx_launch_gen_seek(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
+                               int64_t d, uint64_t* st_out, uint64_t* lab_out, hipStream_t st) {
+    if (B == 0) return hipSuccess;
+    return launch_wave<1>(base_seed, T_seed, run0, B, B, 0, d, 1, 2, 0, nullptr, nullptr,
+                          nullptr, st_out, nullptr, lab_out, st);
+}
+
+hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const uint64_t* st_in,
+                                   uint64_t* st_out, const uint64_t* lab_in, uint64_t* lab_out,
+                                   double* zt, double* ytl, hipStream_t st) {
+    const int64_t nseq = L->G * L->S;
+    if (nseq == 0 || L->T == 0) return hipSuccess;
+    return launch_wave<0>(0, T_seed, 0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt, ytl, st_in,
+                          st_out, lab_in, lab_out, st);
+}

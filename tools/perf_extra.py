@@ -45,10 +45,25 @@ def gen(args):
         torch.cuda.empty_cache()
 
 
+def gen1(args):
+    """One generation config, for PMC passes (rocprofv3 --pmc ... -- python tools/perf_extra.py gen1)."""
+    from online_convex_optimization_amd import engine
+    db = engine.DeviceBatch(65536, 2000, 64, lanes_per_seq=1)
+    for _ in range(2):
+        db.generate_gT(0, 0)
+        sync()
+    t0 = time.perf_counter()
+    db.generate_gT(0, 0)
+    sync()
+    tg = time.perf_counter() - t0
+    print(json.dumps({"what": "gen1", "B": 65536, "T": 2000, "d": 64, "gen_s": tg,
+                      "normals_per_s": 65536 * 2000 * 64 / tg}), flush=True)
+
+
 def sweep(args):
     from online_convex_optimization_amd import engine
     for T, runs in ((100, 1000000), (1000, 1000000), (10000, 131072), (100000, 131072)):
-        engine.gT_regrets(T, 64, d=64, lanes_per_seq=1)  # warm
+        engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)  # warm (incl. the HBM buffers)
         t0 = time.perf_counter()
         regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
         dt = time.perf_counter() - t0
@@ -127,7 +142,7 @@ def smart(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["gen", "sweep", "driver", "smart", "config3", "exact_driver"])
+    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver"])
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
