@@ -63,10 +63,20 @@ __device__ __forceinline__ uint64_t lowmask(int n) {
     return n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL);
 }
 __device__ __forceinline__ uint64_t xsl_rr(ocx_u128 s) {
+    // rotr64(hi ^ lo, hi >> 58) as two funnel shifts (v_alignbit_b32)
     const uint64_t hi = (uint64_t)(s >> 64), lo = (uint64_t)s;
-    const unsigned rot = (unsigned)(hi >> 58);
+    const uint32_t rot = (uint32_t)(hi >> 58);
     const uint64_t x = hi ^ lo;
-    return (x >> rot) | (x << ((0u - rot) & 63u));
+    const uint32_t xl = (uint32_t)x, xh = (uint32_t)(x >> 32);
+    const bool sw = rot & 32;
+    const uint32_t a = sw ? xh : xl, b = sw ? xl : xh;
+    const uint32_t rl = __builtin_amdgcn_alignbit(b, a, rot);
+    const uint32_t rh = __builtin_amdgcn_alignbit(a, b, rot);
+    return ((uint64_t)rh << 32) | rl;
+}
+// (double)v for v < 2^52, exactly: the bits of 2^52 + v, minus 2^52
+__device__ __forceinline__ double u52_to_double(uint64_t v) {
+    return __longlong_as_double((long long)(0x4330000000000000ULL | v)) - 4503599627370496.0;
 }
 __device__ __forceinline__ double u53(uint64_t r) {
     return (double)(r >> 11) * (1.0 / 9007199254740992.0);
@@ -126,7 +136,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const int idx = (int)(r & 0xff);
     const uint64_t r8 = r >> 8;
     const uint64_t rabs = (r8 >> 1) & kMask52;
-    double x = (double)rabs * tb.wi[idx];
+    double x = u52_to_double(rabs) * tb.wi[idx];
     if (r8 & 1) x = -x;
     const bool fast = rabs < tb.ki[idx];
     const uint64_t rej = ballot(!fast);
@@ -200,18 +210,33 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 }
 
 // NumPy pairwise sum of v*v over one leaf of n <= 128 ring values starting at o.
-__device__ __forceinline__ double leaf_sumsq(const double* ring, int rmask, unsigned o, int n,
+// Lane k (mod 8) keeps accumulator r_k = v_k² + v_{k+8}² + ... in order; the loads of
+// a lane are issued together (NF > 0: n known at compile time).
+template <int NF>
+__device__ __forceinline__ double leaf_sumsq(const double* ring, int rmask, unsigned o, int n_arg,
                                              int lane) {
+    const int n = NF ? NF : n_arg;
     double res = 0.0;
     int i = 0;
     if (n >= 8) {
         const int n8 = n - (n % 8);
-        const int k = lane & 7;
-        double v = ring[(o + k) & rmask];
-        double acc = v * v;
-        for (int j = k + 8; j < n8; j += 8) {
-            v = ring[(o + j) & rmask];
-            acc += v * v;
+        const unsigned ok = o + (unsigned)(lane & 7);
+        double acc;
+        if constexpr (NF >= 8) {
+            constexpr int M = (NF - NF % 8) / 8;
+            double v[M];
+#pragma unroll
+            for (int q = 0; q < M; ++q) v[q] = ring[(ok + 8u * q) & rmask];
+            acc = v[0] * v[0];
+#pragma unroll
+            for (int q = 1; q < M; ++q) acc += v[q] * v[q];
+        } else {
+            double v = ring[ok & rmask];
+            acc = v * v;
+            for (int j = 8; j < n8; j += 8) {
+                v = ring[(ok + (unsigned)j) & rmask];
+                acc += v * v;
+            }
         }
         res = ocx_seq_sum<8>(acc);  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) in every lane
         i = n8;
@@ -235,7 +260,7 @@ struct PwFrame {
 
 __device__ double row_sumsq(const double* ring, int rmask, unsigned o, int d, int lane,
                             PwFrame* stk) {
-    if (d <= 128) return leaf_sumsq(ring, rmask, o, d, lane);
+    if (d <= 128) return leaf_sumsq<0>(ring, rmask, o, d, lane);
     int sp = 0;
     if (lane == 0) stk[0] = PwFrame{o, d, 0, 0.0};
     double ret = 0.0;
@@ -243,7 +268,7 @@ __device__ double row_sumsq(const double* ring, int rmask, unsigned o, int d, in
         __builtin_amdgcn_wave_barrier();
         const PwFrame f = stk[sp];
         if (f.n <= 128) {
-            ret = leaf_sumsq(ring, rmask, f.o, f.n, lane);
+            ret = leaf_sumsq<0>(ring, rmask, f.o, f.n, lane);
         } else if (f.state < 2) {
             int n2 = f.n / 2;
             n2 -= n2 % 8;
@@ -282,8 +307,13 @@ __device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, 
 }
 
 constexpr int kWaveBlock = 256;
+// Waves per SIMD the register allocation must allow.  For the d = 64 kernel 6 waves
+// (80 VGPRs, a few cold spills) measured 6 % faster than the unconstrained 104 VGPRs
+// (4 waves); its LDS (6 KB tables + 4 x 4 KB rings per block) also admits 6.
 #ifndef OCX_GENW_MIN_WAVES
-#define OCX_GENW_MIN_WAVES 1  // waves per SIMD the register allocation must allow
+#define OCX_GENW_MIN_WAVES_FOR(DF) ((DF) == 64 ? 6 : 1)
+#else
+#define OCX_GENW_MIN_WAVES_FOR(DF) OCX_GENW_MIN_WAVES
 #endif
 
 // rows per batch leaving the ring (see the kernel)
@@ -302,10 +332,12 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 //   and labels from lab_in[b] (saved to lab_out[b]).
 // MODE 1 (seek): st_out[b] = the fresh stream, lab_out[b] = the stream after its
 //   T_seed·d normals, i.e. where choice(T) starts.
-template <int MODE>
-__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_kernel(
+// DF = 64: the d = 64, P·C = 64 rows of every configs[] workload, with the row shape
+// known at compile time; DF = 0: any d.
+template <int MODE, int DF>
+__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
-    int d, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
+    int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
     const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out, int rb,
     int64_t nwaves) {
@@ -320,7 +352,8 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_k
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6);
     if (wave >= nwaves) return;
-    double* ring = rings + (threadIdx.x >> 6) * (rb + kStackDoubles);
+    const int slot = rb + (d_arg > 128 ? kStackDoubles : 0);  // ring (+ pairwise stack)
+    double* ring = rings + (threadIdx.x >> 6) * slot;
     PwFrame* stk = reinterpret_cast<PwFrame*>(ring + rb);
     const int rmask = rb - 1;
 
@@ -335,8 +368,9 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_k
         }
         w.Ak = a;
     }
+    const int d = DF ? DF : d_arg;
     const int S = 64 / P;
-    const int Dp = P * C;
+    const int Dp = DF ? 64 : P * C;
     // rows leave the ring in batches of R: the sums of squares of a batch run side by
     // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
     const int R = batch_rows(d);
@@ -375,7 +409,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_k
 
         // ---- rows
         const int64_t rows = (MODE == 0) ? T : T_seed;
-        int64_t remaining = rows * d;  // normals still to draw
+        uint32_t remaining = (uint32_t)(rows * d);  // normals still to draw (< 2^32, host-checked)
         unsigned head = 0, tailp = 0;  // ring counters (mod 2^32; masked on use)
         unsigned partial = 0;          // normals of the row being filled
         int ready = 0;                 // whole rows waiting in the ring
@@ -384,7 +418,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_k
             const int need = remaining < 64 ? (int)remaining : 64;
             const int n = zig_round<MODE == 0>(w, need, tb, ring, rmask, head, lane);
             head += n;
-            remaining -= n;
+            remaining -= (uint32_t)n;
             if (MODE != 0) continue;
             partial += (unsigned)n;
             while (partial >= (unsigned)d) {
@@ -405,7 +439,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES) void ocx_gen_wave_k
                             ss += v * v;
                         }
                     } else {
-                        ss = leaf_sumsq(ring, rmask, o, d, lane);
+                        ss = leaf_sumsq<DF>(ring, rmask, o, d, lane);
                     }
                     const double nrm = sqrt(ss);
                     sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
@@ -504,30 +538,45 @@ int ring_doubles(int64_t d) {
     return rb;
 }
 
-template <int MODE>
-hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq,
-                       int64_t T, int64_t d, int P, int C, int64_t G, double* zt, double* ytl,
-                       const uint64_t* st_in, uint64_t* st_out, const uint64_t* lab_in,
-                       uint64_t* lab_out, hipStream_t st) {
+template <int MODE, int DF>
+hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
+                          int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
+                          double* ytl, const uint64_t* st_in, uint64_t* st_out,
+                          const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
     const int rb = (MODE == 0) ? ring_doubles(d) : 0;
-    const size_t lds = (MODE == 0) ? (size_t)(rb + kStackDoubles) * 8 * (kWaveBlock / 64) : 0;
+    const size_t lds =
+        (MODE == 0) ? (size_t)(rb + (d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
     // resident waves: fill the GPU once, sequences spread evenly over the waves
     int dev = 0, cus = 256, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF>,
                                                      kWaveBlock, lds);
     if (e != hipSuccess) return e;
     const int64_t resident = std::max<int64_t>(1, (int64_t)cus * std::max(per_cu, 1) * (kWaveBlock / 64));
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
     const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));
-    hipLaunchKernelGGL(ocx_gen_wave_kernel<MODE>, dim3(blocks), dim3(kWaveBlock), lds, st,
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF>), dim3(blocks), dim3(kWaveBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
                        st_out, lab_in, lab_out, rb, nwaves);
     return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq,
+                       int64_t T, int64_t d, int P, int C, int64_t G, double* zt, double* ytl,
+                       const uint64_t* st_in, uint64_t* st_out, const uint64_t* lab_in,
+                       uint64_t* lab_out, hipStream_t st) {
+    // the kernel counts a sequence's normals in 32 bits
+    if ((MODE == 0 ? T : T_seed) * d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    if (d == 64 && (MODE == 1 || (int64_t)P * C == 64))
+        return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
+                                        st_in, st_out, lab_in, lab_out, st);
+    return launch_wave_df<MODE, 0>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
+                                   st_in, st_out, lab_in, lab_out, st);
 }
 
 }  // namespace

@@ -14,6 +14,9 @@
 // butterfly (ocx_seq_sum).
 #include <algorithm>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "ocx_device_math.h"
 #include "ocx_dispatch.h"
 #include "ocx_internal.h"
@@ -396,6 +399,13 @@ hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double*
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st) {
     if (L->G == 0) return hipSuccess;
+    // Small batches (the drivers' few hundred sequences) cannot hide the prefix
+    // re-scan's latency with lane groups: one wavefront per sequence instead.
+    // OCX_SMART_KERNEL=wave|lanes forces a path (tests, tuning).
+    bool wave = L->d <= 64 && L->B <= 4096;  // measured crossover ≈ 6500 sequences (d = 5)
+    if (const char* e = std::getenv("OCX_SMART_KERNEL"))
+        wave = std::strcmp(e, "wave") == 0 && L->d <= 64;
+    if (wave) return ocx_launch_smart_wave(L, zt, yt, th, eta0, reg, sw, st);
     OCX_DISPATCH(launch_smart_cp, L, zt, yt, th, eta0, reg, sw, st)
 }
 

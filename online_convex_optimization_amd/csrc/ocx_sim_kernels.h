@@ -14,6 +14,10 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);
+// SMART with one wavefront per sequence (ocx_smart_wave.hip), d <= 64
+hipError_t ocx_launch_smart_wave(const ocx_layout* L, const double* zt, const double* yt,
+                                 const double* th, double eta0, double* reg, int64_t* sw,
+                                 hipStream_t st);
 hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double* yt,
                              const double* at, double* cum, double* comp, hipStream_t st);
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,

@@ -1,0 +1,147 @@
+// ocx_smart_wave.hip — SMART (fast_algorithms.py:118-164) with one wavefront per
+// sequence, for batches too small to fill the GPU with the lane-group kernel.
+//
+// SMART's cost is the prefix re-scan before the switch: at every step t it sums
+// ½|z_i·s_t − y_i| over i = 0..t in order, O(T²) dependent additions per sequence.
+// The lane-group kernel (ocx_sim.hip) walks that prefix with one lane group per
+// sequence, so a driver-sized batch (a few hundred sequences) leaves the GPU idle on
+// the latency of every term.  Here the 64 lanes compute 64 terms of the prefix at
+// once (their dot products are independent) and the wave adds them to the running
+// sum in order from LDS, so only the additions themselves stay sequential — the
+// reference's own summation order, bit for bit.  Lane j < d keeps coordinate j of the
+// FTL and FTRL states; the d-term sums of the actions use the same ordered adder.
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+constexpr int kSmartBlock = 256;
+
+// acc + v_0 + v_1 + ... + v_{n-1}, left to right (v_k = lane k's value), n <= 64.
+// The values go through the wave's LDS slot `buf`; every lane returns the same sum.
+__device__ __forceinline__ double ordered_sum(double acc, double v, int n, double* buf,
+                                              int lane) {
+    buf[lane] = v;
+    __builtin_amdgcn_wave_barrier();
+    int k = 0;
+    for (; k + 8 <= n; k += 8) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = buf[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; k < n; ++k) acc += buf[k];
+    __builtin_amdgcn_wave_barrier();
+    return acc;
+}
+
+__device__ __forceinline__ double grad(double diff) {
+    return diff > 0.0 ? 0.5 : (diff < 0.0 ? -0.5 : 0.0);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kSmartBlock) void ocx_smart_wave_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T, int d,
+    int P, int C, int64_t G, const double* __restrict__ thresh, double eta0,
+    double* __restrict__ regret, int64_t* __restrict__ switch_step) {
+    __shared__ double bufs[kSmartBlock];
+    const int lane = threadIdx.x & 63;
+    double* buf = bufs + (threadIdx.x & ~63);
+    const int64_t b = (int64_t)blockIdx.x * (kSmartBlock / 64) + (threadIdx.x >> 6);
+    if (b >= B) return;
+    const int S = 64 / P;
+    const int64_t g = b / S;
+    const int s = (int)(b - g * S);
+    const bool own = lane < d;  // this lane's coordinate j = lane exists
+    // tile offset of coordinate `lane` of this sequence at step 0 (+ t·128 for step t)
+    int64_t zoff = 0;
+    if (own) {
+        const int c = lane / C, rr = lane - c * C;
+        zoff = ((int64_t)(rr >> 1) * G + g) * T * 128 + (s * P + c) * 2 + (rr & 1);
+    }
+    const double* __restrict__ yp = yt + g * T * S + s;  // y_t = yp[t * S]
+    const double th_sw = thresh[b];
+
+    // ½|z_i·sv − y_i| summed over rows i < n in order: lane ℓ forms the terms of rows
+    // i0 + ℓ (coordinates read from the lanes that own them), the wave adds them.
+    auto prefix_loss = [&](double sv, int64_t n) -> double {
+        double tot = 0.0;
+        for (int64_t i0 = 0; i0 < n; i0 += 64) {
+            const int m = (int)((n - i0) < 64 ? (n - i0) : 64);
+            const int64_t i = i0 + (lane < m ? lane : 0);
+            double q = 0.0;
+            for (int j = 0; j < d; ++j) {
+                const int64_t oj = ((int64_t)__builtin_amdgcn_readlane((int)(zoff >> 32), j) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)zoff, j);
+                const double sj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), j),
+                                                   __builtin_amdgcn_readlane(__double2loint(sv), j));
+                q += zt[oj + i * 128] * sj;
+            }
+            const double h = 0.5 * fabs(q - yp[i * S]);
+            tot = ordered_sum(tot, h, m, buf, lane);
+        }
+        return tot;
+    };
+    // FTL action (fast_algorithms.py:37-49) of the state held in `th`, coordinate `lane`
+    auto action_ftl = [&](double th) -> double {
+        const double n2 = ordered_sum(0.0, own ? th * th : 0.0, d, buf, lane);
+        if (n2 == 0.0) return 0.0;
+        const double scale = -(1.0 / sqrt(n2));
+        return scale * th;
+    };
+
+    double tf = 0.0, tr = 0.0;  // theta_ftl, theta_ftrl (coordinate `lane`)
+    bool switched = false;
+    int64_t sw = -1;
+    double ftl_loss = 0.0, total_loss = 0.0;
+    for (int64_t t = 0; t < T; ++t) {
+        const double z = own ? zt[zoff + t * 128] : 0.0;
+        const double yv = yp[t * S];
+        // FTL is always run and updated (:140-146)
+        const double xf = action_ftl(tf);
+        const double pf = ordered_sum(0.0, own ? z * xf : 0.0, d, buf, lane);
+        const double dfl = pf - yv;
+        tf += grad(dfl) * z;
+        const double loss_ftl = 0.5 * fabs(dfl);
+        ftl_loss += loss_ftl;
+        if (switched) {
+            // post-switch: FTRL with its own theta and the global t (:148-154)
+            const double sc = -(eta0 / sqrt((double)(t + 1)));
+            double xr = sc * tr;
+            const double n2 = ordered_sum(0.0, own ? xr * xr : 0.0, d, buf, lane);
+            if (n2 > 1.0) xr *= 1.0 / sqrt(n2);
+            const double pr = ordered_sum(0.0, own ? z * xr : 0.0, d, buf, lane);
+            const double dr = pr - yv;
+            total_loss += 0.5 * fabs(dr);
+            tr += grad(dr) * z;
+        } else {
+            total_loss += loss_ftl;  // :156
+            // s_t = FTL(theta_ftl) after the update; its loss over rows 0..t (:157-160)
+            const double sv = action_ftl(tf);
+            const double s_loss = prefix_loss(sv, t + 1);
+            if (ftl_loss - s_loss >= th_sw) {
+                switched = true;
+                sw = t;
+            }
+        }
+    }
+    // final comparator = FTL(theta_ftl) (:162-163)
+    const double comp = prefix_loss(action_ftl(tf), T);
+    if (lane == 0) {
+        regret[b] = total_loss - comp;
+        if (switch_step) switch_step[b] = sw;
+    }
+}
+
+hipError_t ocx_launch_smart_wave(const ocx_layout* L, const double* zt, const double* yt,
+                                 const double* th, double eta0, double* reg, int64_t* sw,
+                                 hipStream_t st) {
+    if (L->B == 0) return hipSuccess;
+    if (L->d > 64) return hipErrorNotSupported;
+    const unsigned grid = (unsigned)((L->B + (kSmartBlock / 64) - 1) / (kSmartBlock / 64));
+    hipLaunchKernelGGL(ocx_smart_wave_kernel, dim3(grid), dim3(kSmartBlock), 0, st, zt, yt, L->B,
+                       L->T, (int)L->d, L->P, L->C, L->G, th, eta0, reg, sw);
+    return hipGetLastError();
+}

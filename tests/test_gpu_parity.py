@@ -184,19 +184,27 @@ def test_batch_all_lane_splits(ocx, T, d):
             assert close(regc, refc[0]) and close(compc, refc[2]), P
 
 
-def test_smart_batch_splits(ocx):
+@pytest.mark.parametrize("kernel", ["lanes", "wave"])
+@pytest.mark.parametrize("B,T,d", [(19, 120, 12), (70, 200, 5), (5, 130, 64), (3, 0, 4),
+                                   (9, 65, 1)])
+def test_smart_batch_splits(ocx, monkeypatch, kernel, B, T, d):
+    """Both SMART kernels (lane groups / one wave per sequence) against the oracle,
+    thresholds spread so that some sequences switch early, late or never."""
     eng = ocx["engine"]
-    rng = np.random.default_rng(5)
-    B, T, d = 19, 120, 12
+    monkeypatch.setenv("OCX_SMART_KERNEL", kernel)
+    rng = np.random.default_rng(5 + d)
     z = rng.standard_normal((B, T, d))
     z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
     y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
     th = rng.uniform(-1.0, 6.0, size=B)
     ref, sw = O.simulate_smart_batch(z, y, th, SQ2, nthreads=4)
+    assert T == 0 or len(set(sw.tolist())) > 1  # a mix of switch steps
     for P in (1, -1, -4, 2, 4, 8, 64):
+        if d > 64 * abs(P) or (P < -1 and -P > 64):
+            continue
         got, gsw = eng.simulate_smart_batch(z, y, th, SQ2, lanes_per_seq=P, return_switch=True)
-        if P == 1 or P < 0:
-            assert np.array_equal(got, ref) and np.array_equal(gsw, sw)
+        if P == 1 or P < 0 or kernel == "wave":  # the wave kernel always sums in order
+            assert np.array_equal(got, ref) and np.array_equal(gsw, sw), P
         else:
             assert close(got, ref), P
 

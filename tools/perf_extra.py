@@ -124,20 +124,31 @@ def exact_driver(args):
 
 
 def smart(args):
+    """SMART on the driver's batch shape (768 iid sequences, d=5, T=1000) and a large
+    batch, through both kernels (OCX_SMART_KERNEL=lanes|wave)."""
+    import os
     from online_convex_optimization_amd import engine
-    import torch
-    B, T = 768, 1000
-    db = engine.DeviceBatch(B, T, 5, lanes_per_seq=1)
-    db.generate_family("iid", 2025 * (1 + np.repeat(np.arange(48), 16)),
-                       13 + np.tile(np.arange(16), 48))
-    db.simulate_smart(math.sqrt(2 * T))
-    sync()
-    t0 = time.perf_counter()
-    db.simulate_smart(math.sqrt(2 * T))
-    sync()
-    dt = time.perf_counter() - t0
-    print(json.dumps({"what": "smart", "B": B, "T": T, "d": 5, "seconds": dt,
-                      "timesteps_per_s": B * T / dt}), flush=True)
+    for B, T, d in ((768, 1000, 5), (32768, 1000, 5), (768, 1000, 64)):
+        db = engine.DeviceBatch(B, T, d, lanes_per_seq=1)
+        if d == 5:
+            n = B // 16
+            db.generate_family("iid", 2025 * (1 + np.repeat(np.arange(n), 16)),
+                               13 + np.tile(np.arange(16), n))
+        else:
+            db.generate_gT(0, 0)
+        for kern in ("lanes", "wave"):
+            os.environ["OCX_SMART_KERNEL"] = kern
+            r0 = db.simulate_smart(math.sqrt(2 * T)).clone()
+            sync()
+            t0 = time.perf_counter()
+            r = db.simulate_smart(math.sqrt(2 * T))
+            sync()
+            dt = time.perf_counter() - t0
+            print(json.dumps({"what": "smart", "kernel": kern, "B": B, "T": T, "d": d,
+                              "seconds": dt, "timesteps_per_s": B * T / dt,
+                              "same_as_first": bool((r == r0).all())}), flush=True)
+        os.environ.pop("OCX_SMART_KERNEL", None)
+        del db
 
 
 if __name__ == "__main__":
