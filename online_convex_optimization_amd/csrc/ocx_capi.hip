@@ -436,16 +436,20 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB, default 64 GiB)
     int64_t budget = (int64_t)64 << 30;
     if (const char* e = std::getenv("OCX_HBM_BUDGET_GB")) budget = (int64_t)(std::atof(e) * (1 << 30));
-    const int64_t kBatch = 131072;  // concurrent streams that fill the generator
+    const int64_t kBatch = 131072;   // streams per batch of the streamed path
+    const int64_t kMinResident = 8192;  // a resident batch must fill the generator and the FTRL kernel
     ocx_layout L1;
     if (int rc = ocx_layout_init(std::min<int64_t>(R, kBatch), std::max<int64_t>(T, 1), d,
                                  lanes_per_seq, &L1))
         return rc;
     const int64_t step_bytes = (L1.z_elems + L1.y_elems) * 8 / std::max<int64_t>(T, 1);
-    const bool streamed = step_bytes * T > budget && L1.Dp <= 64;
+    // whole horizon of one sequence, resident
+    const int64_t per_seq = std::max<int64_t>(step_bytes * T / std::max<int64_t>(L1.B, 1), 8);
+    // Resident batches (generate once, simulate once) while a batch still holds enough
+    // sequences; otherwise stream the horizon (seek + two generation passes).
+    const bool streamed = budget / per_seq < std::min<int64_t>(R, kMinResident);
     if (!streamed) {
         // whole horizon resident: as many runs per batch as the budget holds
-        const int64_t per_seq = std::max<int64_t>(step_bytes * T / std::max<int64_t>(L1.B, 1), 8);
         int64_t chunk = std::max<int64_t>(64, std::min<int64_t>(budget / per_seq, R));
         OCX_HIP(cx->out.ensure((size_t)chunk * 8));
         for (int64_t r0 = 0; r0 < R; r0 += chunk) {

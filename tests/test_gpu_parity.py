@@ -312,7 +312,8 @@ def test_driver_stats_golden(ocx, golden):
 
 
 # ------------------------------------------------------------------ long-horizon (chunked)
-@pytest.mark.parametrize("T,d,runs,P", [(300, 5, 100, 1), (257, 64, 40, 0), (1000, 16, 70, -1)])
+@pytest.mark.parametrize("T,d,runs,P", [(300, 5, 100, 1), (257, 64, 40, 0), (1000, 16, 70, -1),
+                                         (130, 100, 20, 0), (37, 1024, 6, 0), (211, 64, 33, 1)])
 def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
     """A tiny HBM budget forces the T-chunked path (seek → pass A → pass B with saved PCG
     states): regrets must equal the single-launch path bit for bit."""
