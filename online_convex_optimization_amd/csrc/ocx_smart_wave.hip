@@ -42,6 +42,7 @@ __device__ __forceinline__ double grad(double diff) {
 
 }  // namespace
 
+template <int DMAX>
 __global__ __launch_bounds__(kSmartBlock) void ocx_smart_wave_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T, int d,
     int P, int C, int64_t G, const double* __restrict__ thresh, double eta0,
@@ -65,22 +66,50 @@ __global__ __launch_bounds__(kSmartBlock) void ocx_smart_wave_kernel(
     const double th_sw = thresh[b];
 
     // ½|z_i·sv − y_i| summed over rows i < n in order: lane ℓ forms the terms of rows
-    // i0 + ℓ (coordinates read from the lanes that own them), the wave adds them.
+    // i0 + ℓ (coordinates read from the lanes that own them), the wave adds them.  With
+    // DMAX > 0 (d <= DMAX) the next chunk's rows are loaded while this chunk is summed.
+    auto offset_of = [&](int j) -> int64_t {
+        return ((int64_t)__builtin_amdgcn_readlane((int)(zoff >> 32), j) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)zoff, j);
+    };
+    auto coord_of = [&](double v, int j) -> double {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), j),
+                                __builtin_amdgcn_readlane(__double2loint(v), j));
+    };
     auto prefix_loss = [&](double sv, int64_t n) -> double {
         double tot = 0.0;
-        for (int64_t i0 = 0; i0 < n; i0 += 64) {
-            const int m = (int)((n - i0) < 64 ? (n - i0) : 64);
-            const int64_t i = i0 + (lane < m ? lane : 0);
-            double q = 0.0;
-            for (int j = 0; j < d; ++j) {
-                const int64_t oj = ((int64_t)__builtin_amdgcn_readlane((int)(zoff >> 32), j) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane((int)zoff, j);
-                const double sj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), j),
-                                                   __builtin_amdgcn_readlane(__double2loint(sv), j));
-                q += zt[oj + i * 128] * sj;
+        if constexpr (DMAX > 0) {
+            double zc[DMAX], yc = 0.0;
+            auto load = [&](int64_t i0, double (&zb)[DMAX], double& yb) {
+                const int64_t i = (i0 + lane < n) ? i0 + lane : 0;
+#pragma unroll
+                for (int j = 0; j < DMAX; ++j) zb[j] = (j < d) ? zt[offset_of(j) + i * 128] : 0.0;
+                yb = yp[i * S];
+            };
+            if (n > 0) load(0, zc, yc);
+            for (int64_t i0 = 0; i0 < n; i0 += 64) {
+                const int m = (int)((n - i0) < 64 ? (n - i0) : 64);
+                double zn[DMAX], yn = 0.0;
+                if (i0 + 64 < n) load(i0 + 64, zn, yn);
+                double q = 0.0;
+#pragma unroll
+                for (int j = 0; j < DMAX; ++j)
+                    if (j < d) q += zc[j] * coord_of(sv, j);
+                const double h = 0.5 * fabs(q - yc);
+                tot = ordered_sum(tot, h, m, buf, lane);
+#pragma unroll
+                for (int j = 0; j < DMAX; ++j) zc[j] = zn[j];
+                yc = yn;
             }
-            const double h = 0.5 * fabs(q - yp[i * S]);
-            tot = ordered_sum(tot, h, m, buf, lane);
+        } else {
+            for (int64_t i0 = 0; i0 < n; i0 += 64) {
+                const int m = (int)((n - i0) < 64 ? (n - i0) : 64);
+                const int64_t i = i0 + (lane < m ? lane : 0);
+                double q = 0.0;
+                for (int j = 0; j < d; ++j) q += zt[offset_of(j) + i * 128] * coord_of(sv, j);
+                const double h = 0.5 * fabs(q - yp[i * S]);
+                tot = ordered_sum(tot, h, m, buf, lane);
+            }
         }
         return tot;
     };
@@ -141,7 +170,11 @@ hipError_t ocx_launch_smart_wave(const ocx_layout* L, const double* zt, const do
     if (L->B == 0) return hipSuccess;
     if (L->d > 64) return hipErrorNotSupported;
     const unsigned grid = (unsigned)((L->B + (kSmartBlock / 64) - 1) / (kSmartBlock / 64));
-    hipLaunchKernelGGL(ocx_smart_wave_kernel, dim3(grid), dim3(kSmartBlock), 0, st, zt, yt, L->B,
-                       L->T, (int)L->d, L->P, L->C, L->G, th, eta0, reg, sw);
+    if (L->d <= 8)
+        hipLaunchKernelGGL(ocx_smart_wave_kernel<8>, dim3(grid), dim3(kSmartBlock), 0, st, zt, yt,
+                           L->B, L->T, (int)L->d, L->P, L->C, L->G, th, eta0, reg, sw);
+    else
+        hipLaunchKernelGGL(ocx_smart_wave_kernel<0>, dim3(grid), dim3(kSmartBlock), 0, st, zt, yt,
+                           L->B, L->T, (int)L->d, L->P, L->C, L->G, th, eta0, reg, sw);
     return hipGetLastError();
 }
