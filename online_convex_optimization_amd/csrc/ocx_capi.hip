@@ -137,9 +137,12 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
         P = (int)std::max(p_min, std::min(p_lanes, p_max));
     } else if (lanes_per_seq == 1) {
         // exact auto: at most 16 coordinates per lane (register budget of the chained
-        // sums), then up to 4 lanes while that is needed to reach 65536 lanes.
+        // sums; 32 from d = 512 on, where the chain's hop count costs more than the
+        // registers: d = 1024 measured 1.6x faster at 32 lanes x 32 than 64 x 16), then
+        // up to 4 lanes while that is needed to reach 65536 lanes.
+        const int64_t cmax = d >= 512 ? 32 : 16;
         int64_t p = 1;
-        while (p < 64 && ceil_div(d, p) > 16) p *= 2;
+        while (p < 64 && ceil_div(d, p) > cmax) p *= 2;
         while (p < 4 && p * B < 65536 && ceil_div(d, 2 * p) >= 2) p *= 2;
         P = (int)p;
     }

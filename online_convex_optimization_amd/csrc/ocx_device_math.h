@@ -55,17 +55,54 @@ __device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
         for (int j = 0; j < C; ++j) acc += p[j];
         return ocx_seq_sum<P>(acc);
     } else {
+        // the running sum moves one lane up per hop (DPP wave_shr:1, lane i <- lane i-1:
+        // a VALU move, no LDS round trip); the group's last lane then holds the total,
+        // which one bpermute hands to all P lanes
         const int c = lane % P;
-        const int base = lane - c;
         double acc = 0.0;
         for (int cc = 0; cc < P; ++cc) {
             if (c == cc) {
 #pragma unroll
                 for (int j = 0; j < C; ++j) acc += p[j];
             }
-            acc = __shfl(acc, base + cc, 64);
+            if (cc + 1 < P) acc = ocx_dpp<0x138>(acc);
         }
-        return acc;
+        return __shfl(acc, lane - c + P - 1, 64);
+    }
+}
+
+// Two independent totals at once (same order as two ocx_total calls): their chains /
+// butterflies interleave, so the second one rides on the first one's latency.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ void ocx_total2(const double (&p)[C], const double (&q)[C], double& a,
+                                           double& b, int lane) {
+    if constexpr (!CHAIN || P == 1) {
+        double x = 0.0, y = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            x += p[j];
+            y += q[j];
+        }
+        a = ocx_seq_sum<P>(x);
+        b = ocx_seq_sum<P>(y);
+    } else {
+        const int c = lane % P;
+        double x = 0.0, y = 0.0;
+        for (int cc = 0; cc < P; ++cc) {
+            if (c == cc) {
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    x += p[j];
+                    y += q[j];
+                }
+            }
+            if (cc + 1 < P) {
+                x = ocx_dpp<0x138>(x);
+                y = ocx_dpp<0x138>(y);
+            }
+        }
+        a = __shfl(x, lane - c + P - 1, 64);
+        b = __shfl(y, lane - c + P - 1, 64);
     }
 }
 
@@ -100,6 +137,36 @@ __device__ __forceinline__ void ocx_action_ftl(const double (&th)[C], double (&x
     const double sc = -(1.0 / sqrt(nsq));
 #pragma unroll
     for (int j = 0; j < C; ++j) x[j] = (nsq == 0.0) ? 0.0 : sc * th[j];
+}
+
+// FTRL action and q = z_t·x in one pass (fast_algorithms.py:52-66, :105).  ‖sθ‖² and
+// z·(sθ) are summed side by side; when ‖sθ‖² <= 1 the action is sθ itself (the
+// reference's rescale does not happen) and that q is the answer.  Otherwise x is
+// rescaled and q summed again.  Every sum keeps the reference's order.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const ocx_d2* z,
+                                                   int64_t t1, double eta0, double (&x)[C],
+                                                   int lane) {
+    const double sc = -(eta0 / sqrt((double)t1));
+    double p[C], pq[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        x[j] = sc * th[j];
+        p[j] = x[j] * x[j];
+        pq[j] = ((j & 1) ? z[j >> 1].y : z[j >> 1].x) * x[j];
+    }
+    double nsq, q;
+    ocx_total2<C, P, CHAIN>(p, pq, nsq, q, lane);
+    if (nsq > 1.0) {
+        const double f = 1.0 / sqrt(nsq);
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            x[j] *= f;
+            pq[j] = ((j & 1) ? z[j >> 1].y : z[j >> 1].x) * x[j];
+        }
+        q = ocx_total<C, P, CHAIN>(pq, lane);
+    }
+    return q;
 }
 
 template <int C, int P, bool CHAIN>

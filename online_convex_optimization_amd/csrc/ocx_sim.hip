@@ -80,9 +80,13 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
                     yb[(u + NB - 1) % NB] = yp[tp * S];
                 }
                 double x[C];
-                if (!ftl) ocx_action_ftrl<C, P, CHAIN>(th, t + 1, eta0, x, lane);
-                else ocx_action_ftl<C, P, CHAIN>(th, x, lane);
-                const double q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);  // :105
+                double q;  // :105
+                if (!ftl) {
+                    q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t + 1, eta0, x, lane);
+                } else {
+                    ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                    q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
+                }
                 if (x_last != nullptr && t == T - 1 && b < B) {
 #pragma unroll
                     for (int j = 0; j < C; ++j) {

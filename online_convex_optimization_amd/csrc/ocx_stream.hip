@@ -64,9 +64,13 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                         yb[(u + NB - 1) % NB] = yp[tp * S];
                     }
                     double x[C];
-                    if (!ftl) ocx_action_ftrl<C, P, CHAIN>(th, t0 + t + 1, eta0, x, lane);
-                    else ocx_action_ftl<C, P, CHAIN>(th, x, lane);
-                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
+                    double q;
+                    if (!ftl) {
+                        q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t0 + t + 1, eta0, x, lane);
+                    } else {
+                        ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                        q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
+                    }
                     const double diff = q - yb[u];
                     cum += 0.5 * fabs(diff);
                     const double gq = ocx_grad(diff);

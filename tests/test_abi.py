@@ -59,14 +59,16 @@ def test_auto_layout_choices():
     assert _lib.layout(8, 10, 4096).C == 64             # d/P <= 64
     with pytest.raises(_lib.OCXError):
         _lib.layout(1, 10, 5000)
-    ex = _lib.layout(3, 10, 1000, 1)                     # exact mode above 64 coordinates
-    assert (ex.P, ex.C, ex.chain) == (64, 16, 1)
+    ex = _lib.layout(3, 10, 1000, 1)                     # exact mode, d >= 512: 32 coords/lane
+    assert (ex.P, ex.C, ex.chain) == (32, 32, 1)
+    ex = _lib.layout(3, 10, 300, 1)                      # exact mode below: 16 coords/lane
+    assert (ex.P, ex.C, ex.chain) == (32, 16, 1)
     assert _lib.layout(3, 10, 64, -1).chain == 0          # exact, one lane per sequence
     ch = _lib.layout(3, 10, 64, 1)                         # exact, auto lanes: chained
     assert ch.chain == 1 and ch.P == 4 and ch.C == 16
     assert (_lib.layout(65536, 10, 16, 1).P, _lib.layout(65536, 10, 16, 1).chain) == (1, 0)
     assert _lib.layout(32768, 10, 64, 1).P == 4
-    assert _lib.layout(5, 10, 1024, 1).P == 64
+    assert _lib.layout(5, 10, 1024, 1).P == 32
     assert _lib.layout(3, 10, 5, -4).C == 2 and _lib.layout(3, 10, 5, -4).chain == 1
     assert _lib.layout(3, 10, 12, -2).C == 8                # chain C is a power of two
 
