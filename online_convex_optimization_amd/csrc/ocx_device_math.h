@@ -139,6 +139,14 @@ __device__ __forceinline__ void ocx_action_ftl(const double (&th)[C], double (&x
     for (int j = 0; j < C; ++j) x[j] = (nsq == 0.0) ? 0.0 : sc * th[j];
 }
 
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
+    double p[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * x[j];
+    return ocx_total<C, P, CHAIN>(p, lane);
+}
+
 // FTRL action and q = z_t·x in one pass (fast_algorithms.py:52-66, :105).  ‖sθ‖² and
 // z·(sθ) are summed side by side; when ‖sθ‖² <= 1 the action is sθ itself (the
 // reference's rescale does not happen) and that q is the answer.  Otherwise x is
@@ -148,32 +156,45 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
                                                    int64_t t1, double eta0, double (&x)[C],
                                                    int lane) {
     const double sc = -(eta0 / sqrt((double)t1));
-    double p[C], pq[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) {
-        x[j] = sc * th[j];
-        p[j] = x[j] * x[j];
-        pq[j] = ((j & 1) ? z[j >> 1].y : z[j >> 1].x) * x[j];
-    }
+    for (int j = 0; j < C; ++j) x[j] = sc * th[j];
+    // products formed where they are summed: no p[]/pq[] arrays held across the sums
     double nsq, q;
-    ocx_total2<C, P, CHAIN>(p, pq, nsq, q, lane);
+    if constexpr (!CHAIN || P == 1) {
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            a += x[j] * x[j];
+            b += ocx_zj(z, j) * x[j];
+        }
+        nsq = ocx_seq_sum<P>(a);
+        q = ocx_seq_sum<P>(b);
+    } else {
+        const int c = lane % P;
+        double a = 0.0, b = 0.0;
+        for (int cc = 0; cc < P; ++cc) {
+            if (c == cc) {
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    a += x[j] * x[j];
+                    b += ocx_zj(z, j) * x[j];
+                }
+            }
+            if (cc + 1 < P) {
+                a = ocx_dpp<0x138>(a);
+                b = ocx_dpp<0x138>(b);
+            }
+        }
+        nsq = __shfl(a, lane - c + P - 1, 64);
+        q = __shfl(b, lane - c + P - 1, 64);
+    }
     if (nsq > 1.0) {
         const double f = 1.0 / sqrt(nsq);
 #pragma unroll
-        for (int j = 0; j < C; ++j) {
-            x[j] *= f;
-            pq[j] = ((j & 1) ? z[j >> 1].y : z[j >> 1].x) * x[j];
-        }
-        q = ocx_total<C, P, CHAIN>(pq, lane);
+        for (int j = 0; j < C; ++j) x[j] *= f;
+        q = ocx_zdot<C, P, CHAIN>(z, x, lane);
     }
     return q;
 }
 
-template <int C, int P, bool CHAIN>
-__device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
-    double p[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * x[j];
-    return ocx_total<C, P, CHAIN>(p, lane);
-}
 

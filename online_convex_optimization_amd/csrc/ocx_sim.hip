@@ -33,8 +33,13 @@
 //          (max ||z_t||² <= 1 + 1e-6 and |y_t| == 1); the caller rejects otherwise.
 // cmp_out [B][d] (nullable) receives the comparator action of the second pass.
 // ---------------------------------------------------------------------------
+// Waves per SIMD the register allocation of the FTRL kernel must allow (tuning knob:
+// -DOCX_ALG_MIN_WAVES=2 asks for 2 waves/SIMD when C <= 16).
+#ifndef OCX_ALG_MIN_WAVES
+#define OCX_ALG_MIN_WAVES 1
+#endif
 template <int C, int P, bool CHAIN, int NB>
-__global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_kernel(
+__global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void ocx_alg_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t d, int64_t G, int algo, double eta0, const double* __restrict__ comparator,
     double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
