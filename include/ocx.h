@@ -23,9 +23,9 @@
  *       0      auto: the fewest lanes that fill the GPU; partial sums combined by a
  *              butterfly (~1e-16 relative to the reference's sequential sums);
  *       k >= 2 k lanes (power of two), butterfly sums;
- *       1      exact, auto lanes (<= 16 coordinates per lane, <= 4 lanes unless d
- *              needs more): every sum in the reference's sequential order, so
- *              results are bit-identical;
+ *       1      exact, auto lanes (<= 16 coordinates per lane, <= 32 from d = 512 on;
+ *              <= 4 lanes unless d needs more): every sum in the reference's
+ *              sequential order, so results are bit-identical;
  *       -k     exact with k lanes; for k > 1 the running sum is handed from lane to
  *              lane (layout.chain = 1).
  */
