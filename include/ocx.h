@@ -106,6 +106,19 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
                         int norm, double* cum_loss, double* comp_loss, double* cmp_action,
                         int32_t* regime, int lanes_per_seq, int device);
 
+/* exact_ftl_driver.py:157-186 per sequence, batched, in one read of the data: exact FTL
+ * (as ocx_ftl_exact_batch, l2 closed form) and FTRL (fast_algorithms.py:88-111 order,
+ * eta0) against the exact comparator actions[T] (exact_ftl.py:399-420 run_ftrl with
+ * comparator_action).  Outputs [B]: cum_ftrl, cum_exact, comp_exact (the loss of
+ * actions[T], shared by both regrets: FTRL = cum_ftrl - comp_exact, exact FTL =
+ * cum_exact - comp_exact), comp_ftl (nullable: the loss of FTL(theta_ftrl), the
+ * comparator simulate_alg itself would use), cmp_action [B][d] (nullable) and regime
+ * (int32, required; see ocx_ftl_exact_batch). */
+int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                            double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                            double* comp_ftl, double* cmp_action, int32_t* regime,
+                            int lanes_per_seq, int device);
+
 /* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
  * cum_loss = sum_{t<T} 0.5|z_t.a_t - y_t|; comp_loss = sum_t 0.5|z_t.a_T - y_t|. */
 int ocx_replay_batch(const double* z, const double* y, const double* actions, int64_t B,
@@ -152,6 +165,12 @@ int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const doubl
 int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
                       double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
                       void* stream);
+
+/* ocx_ftrl_vs_exact_batch on device: both loops in one pass, both comparator losses in
+ * a second (two HBM passes instead of four). */
+int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                          double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                          double* comp_ftl, double* cmp_action, int32_t* regime, void* stream);
 
 /* fast_algorithms.py:118-164 on device; thresh [B] device. */
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,

@@ -53,6 +53,11 @@ SIGNATURES = {
                                     ctypes.POINTER(ctypes.c_int32), c_int, c_int]),
     "ocx_dev_ftl_exact": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
                                   c_vp]),
+    "ocx_ftrl_vs_exact_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_double, c_dp, c_dp,
+                                        c_dp, c_dp, c_dp, ctypes.POINTER(ctypes.c_int32), c_int,
+                                        c_int]),
+    "ocx_dev_ftrl_vs_exact": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_replay_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_dp, c_int]),
     "ocx_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp, c_int, c_int]),
     "ocx_dev_pack": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_vp, c_vp]),

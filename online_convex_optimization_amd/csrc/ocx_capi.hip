@@ -242,6 +242,18 @@ int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* 
     return OCX_OK;
 }
 
+int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                          double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                          double* comp_ftl, double* cmp_action, int32_t* regime, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (L->B && (!cum_ftrl || !cum_exact || !comp_exact || !regime))
+        return fail(OCX_E_INVALID, "NULL output buffer");
+    OCX_HIP(ocx_launch_ftrl_exact(L, z_tiled, y_tiled, eta0, cum_ftrl, cum_exact, comp_exact,
+                                  comp_ftl, cmp_action, regime, (hipStream_t)stream));
+    return OCX_OK;
+}
+
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                            const double* thresh, double eta0, double* regret,
                            int64_t* switch_step, void* stream) {
@@ -386,6 +398,45 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
     if (cum_loss) std::memcpy(cum_loss, h.data(), B * 8);
     if (comp_loss) std::memcpy(comp_loss, h.data() + B, B * 8);
     if (cmp_action && d) std::memcpy(cmp_action, h.data() + 2 * B, (size_t)B * d * 8);
+    return OCX_OK;
+}
+
+int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                            double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                            double* comp_ftl, double* cmp_action, int32_t* regime,
+                            int lanes_per_seq, int device) {
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || !cum_ftrl || !cum_exact || !comp_exact || !regime)
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * (4 + d) * 8 + (size_t)B * 4));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    double* o = cx->out.as<double>();
+    int* rg = reinterpret_cast<int*>(o + B * (4 + d));
+    OCX_HIP(ocx_launch_ftrl_exact(&L, cx->zt.as<double>(), cx->yt.as<double>(), eta0, o, o + B,
+                                  o + 2 * B, o + 3 * B, o + 4 * B, rg, st));
+    std::vector<double> h((size_t)B * (4 + d));
+    OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    std::memcpy(cum_ftrl, h.data(), B * 8);
+    std::memcpy(cum_exact, h.data() + B, B * 8);
+    std::memcpy(comp_exact, h.data() + 2 * B, B * 8);
+    if (comp_ftl) std::memcpy(comp_ftl, h.data() + 3 * B, B * 8);
+    if (cmp_action && d) std::memcpy(cmp_action, h.data() + 4 * B, (size_t)B * d * 8);
     return OCX_OK;
 }
 

@@ -1,0 +1,208 @@
+// ocx_ftrl_exact.hip — exact_ftl_driver's per-sequence work (exact_ftl_driver.py:157-186)
+// in one read of the data: FTRL and exact FTL side by side.
+//
+// The driver runs, for every sequence, exact FTL (compute_prefix_actions + replay,
+// exact_ftl.py:280-333) and FTRL against the exact comparator actions[T]
+// (run_ftrl(comparator_action=), exact_ftl.py:399-420).  Both loops consume the same
+// z_t, y_t, and both regrets use the same comparator loss, so one kernel does:
+//   pass 1  FTRL (θ_r, fast_algorithms.py:88-111 order) and exact FTL (θ_e = −S_t, the
+//           closed form of ocx_sim.hip's algo 2, with its regime check) per step;
+//   pass 2  the loss of x* = FTL(θ_e) = S_T/‖S_T‖, and optionally of FTL(θ_r) (the
+//           comparator fast_algorithms.simulate_alg itself would use).
+// Two HBM passes instead of four.  Per step the FTRL sums (‖sθ_r‖², z·sθ_r) and the
+// exact-FTL sums (‖θ_e‖², ‖z‖²) run as one 4-way chain; then z·x_e.
+#include "ocx_device_math.h"
+#include "ocx_dispatch.h"
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+// N per-sequence totals at once; prod(j, k) is product k of this lane's coordinate j.
+// Each total keeps the reference's order (sequential over j, then lane to lane in
+// chain mode; lane-local then the butterfly in tree mode).
+template <int C, int P, bool CHAIN, int N, class F>
+__device__ __forceinline__ void ocx_totals(F&& prod, double (&out)[N], int lane) {
+    double acc[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) acc[k] = 0.0;
+    if constexpr (!CHAIN || P == 1) {
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+#pragma unroll
+            for (int k = 0; k < N; ++k) acc[k] += prod(j, k);
+#pragma unroll
+        for (int k = 0; k < N; ++k) out[k] = ocx_seq_sum<P>(acc[k]);
+    } else {
+        const int c = lane % P;
+        for (int cc = 0; cc < P; ++cc) {
+            if (c == cc) {
+#pragma unroll
+                for (int j = 0; j < C; ++j)
+#pragma unroll
+                    for (int k = 0; k < N; ++k) acc[k] += prod(j, k);
+            }
+            if (cc + 1 < P) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k] = ocx_dpp<0x138>(acc[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < N; ++k) out[k] = __shfl(acc[k], lane - c + P - 1, 64);
+    }
+}
+
+template <int C, int P, bool CHAIN, int NB>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t d, int64_t G, double eta0, double* __restrict__ cum_r, double* __restrict__ cum_e,
+    double* __restrict__ comp_e, double* __restrict__ comp_f, double* __restrict__ cmp_out,
+    int* __restrict__ regime_out) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 64;
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;
+    const double* __restrict__ yp = yt + g * T * S + s;
+
+    double tr[C], te[C];  // θ_ftrl, θ_exact = −S_t
+#pragma unroll
+    for (int j = 0; j < C; ++j) tr[j] = te[j] = 0.0;
+    bool linear = true;
+
+    ocx_d2 zb[NB][K];
+    double yb[NB];
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+            yb[u] = yp[u * S];
+        }
+    double cr = 0.0, ce = 0.0;
+    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+                const int64_t tp = t + NB - 1;
+                if (tp < T) {
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                    yb[(u + NB - 1) % NB] = yp[tp * S];
+                }
+                const ocx_d2* z = zb[u];
+                const double yv = yb[u];
+                // FTRL action terms (fast_algorithms.py:52-66), exact-FTL norm, ‖z_t‖²
+                const double sc = -(eta0 / sqrt((double)(t + 1)));
+                double xr[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) xr[j] = sc * tr[j];
+                double tot[4];
+                ocx_totals<C, P, CHAIN, 4>(
+                    [&](int j, int k) -> double {
+                        const double zj = ocx_zj(z, j);
+                        return k == 0 ? xr[j] * xr[j]
+                                      : (k == 1 ? zj * xr[j] : (k == 2 ? te[j] * te[j] : zj * zj));
+                    },
+                    tot, lane);
+                double qr = tot[1];
+                if (tot[0] > 1.0) {  // FTRL rescale (rare): x *= 1/‖x‖, q again
+                    const double f = 1.0 / sqrt(tot[0]);
+#pragma unroll
+                    for (int j = 0; j < C; ++j) xr[j] *= f;
+                    qr = ocx_zdot<C, P, CHAIN>(z, xr, lane);
+                }
+                // exact FTL: x = FTL(θ_e) (fast_algorithms.py:37-49 form), q = z·x
+                double xe[C];
+                const double sce = -(1.0 / sqrt(tot[2]));
+#pragma unroll
+                for (int j = 0; j < C; ++j) xe[j] = (tot[2] == 0.0) ? 0.0 : sce * te[j];
+                const double qe = ocx_zdot<C, P, CHAIN>(z, xe, lane);
+                const double dr = qr - yv;
+                cr += 0.5 * fabs(dr);
+                ce += 0.5 * fabs(qe - yv);
+                linear = linear && tot[3] <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+                const double gr = ocx_grad(dr);
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const double zj = ocx_zj(z, j);
+                    tr[j] += gr * zj;
+                    te[j] += (-yv) * zj;
+                }
+            }
+        }
+    }
+
+    // ---- pass 2: comparator x* = FTL(θ_e); optionally FTL(θ_r) ----
+    double xs[C], xf[C];
+    ocx_action_ftl<C, P, CHAIN>(te, xs, lane);
+    if (comp_f != nullptr) ocx_action_ftl<C, P, CHAIN>(tr, xf, lane);
+    if (cmp_out != nullptr && b < B) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            const int64_t jj = (int64_t)c * C + j;
+            if (jj < d) cmp_out[b * d + jj] = xs[j];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+            yb[u] = yp[u * S];
+        }
+    double ke = 0.0, kf = 0.0;
+    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+                const int64_t tp = t + NB - 1;
+                if (tp < T) {
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                    yb[(u + NB - 1) % NB] = yp[tp * S];
+                }
+                const ocx_d2* z = zb[u];
+                if (comp_f != nullptr) {
+                    double q2[2];
+                    ocx_totals<C, P, CHAIN, 2>(
+                        [&](int j, int k) -> double { return ocx_zj(z, j) * (k ? xf[j] : xs[j]); },
+                        q2, lane);
+                    ke += 0.5 * fabs(q2[0] - yb[u]);
+                    kf += 0.5 * fabs(q2[1] - yb[u]);
+                } else {
+                    ke += 0.5 * fabs(ocx_zdot<C, P, CHAIN>(z, xs, lane) - yb[u]);
+                }
+            }
+        }
+    }
+    if (c == 0 && b < B) {
+        cum_r[b] = cr;
+        cum_e[b] = ce;
+        comp_e[b] = ke;
+        if (comp_f != nullptr) comp_f[b] = kf;
+        regime_out[b] = linear ? 1 : 0;
+    }
+}
+
+namespace {
+template <int C, int P, bool CH>
+hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt, double eta0,
+                        double* cum_r, double* cum_e, double* comp_e, double* comp_f,
+                        double* cmp_out, int* regime, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C)>),
+                       dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
+                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e,
+                       comp_e, comp_f, cmp_out, regime);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
+                                 double eta0, double* cum_r, double* cum_e, double* comp_e,
+                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    OCX_DISPATCH(launch_fe_cp, L, zt, yt, eta0, cum_r, cum_e, comp_e, comp_f, cmp_out, regime, st)
+}

@@ -36,3 +36,7 @@ hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const ui
 hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                 int64_t t0, int alg_flag, double eta0, int mode, double* theta,
                                 double* cum, double* comp, double* regret, hipStream_t st);
+// FTRL and exact FTL in one pass (ocx_ftrl_exact.hip)
+hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
+                                 double eta0, double* cum_r, double* cum_e, double* comp_e,
+                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st);

@@ -132,12 +132,13 @@ def exact_case_regrets(title: str, T: int, *, runs: int, replicates: int, base_s
 
 
 def _exact_pair(db, B, d, torch) -> Dict[str, np.ndarray]:
-    act = torch.zeros((max(B, 1), d), dtype=torch.float64, device=db.device)
-    regime = db.ftl_exact(cmp_action=act)
-    ftl = (db.cum - db.comp).clone()
+    """Both regrets of exact_ftl_driver.py:169-184 in one read of the batch
+    (ocx_dev_ftrl_vs_exact): FTRL and exact FTL against the exact comparator actions[T]."""
+    regime = db.ftrl_vs_exact(SQRT2)
     if not bool(regime[:B].all()):
         raise NotImplementedError("a sequence left the exact-FTL closed form's regime")
-    ftrl = db.simulate_alg(0, SQRT2, comparator=act).clone()
+    ftrl = db.cum - db.comp
+    ftl = db.cum_exact - db.comp
     return {"FTRL": ftrl[:B].cpu().numpy(), "FTL (exact)": ftl[:B].cpu().numpy()}
 
 

@@ -124,6 +124,37 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: i
     return cum, comp, act, ok
 
 
+def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, device: int = 0,
+                        check_regime: bool = True, with_ftl_comparator: bool = False):
+    """exact_ftl_driver.py:157-186 for B sequences in one read of the data: exact FTL
+    (closed form, as ftl_exact_batch) and FTRL against its comparator actions[T].
+
+    Returns a dict of [B] arrays: ``ftrl`` and ``exact`` regrets, ``cum_ftrl``,
+    ``cum_exact``, ``comp`` (the loss of actions[T], shared by both), ``action``
+    [B, d], ``in_regime``; with ``with_ftl_comparator`` also ``comp_ftl``, the loss of
+    FTL(theta_ftrl) (the comparator simulate_alg itself uses)."""
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    cr, ce, cmp_e, cmp_f = (np.zeros(B) for _ in range(4))
+    act = np.zeros((B, d))
+    rg = np.zeros(B, dtype=np.int32)
+    _lib.call("ocx_ftrl_vs_exact_batch", ptr(z), ptr(y), B, T, d, float(eta0), ptr(cr), ptr(ce),
+              ptr(cmp_e), ptr(cmp_f) if with_ftl_comparator else None, ptr(act),
+              rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
+    ok = rg.astype(bool)
+    if check_regime and not ok.all():
+        bad = int(np.flatnonzero(~ok)[0])
+        raise NotImplementedError(
+            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
+            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+    out = {"ftrl": cr - cmp_e, "exact": ce - cmp_e, "cum_ftrl": cr, "cum_exact": ce,
+           "comp": cmp_e, "action": act, "in_regime": ok}
+    if with_ftl_comparator:
+        out["comp_ftl"] = cmp_f
+    return out
+
+
 def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
                run0: int = 0, lanes_per_seq: int = 0, device: int = 0) -> np.ndarray:
     """Regrets of FTRL on _rng(base_seed, T, run) sequences, run in [run0, run0+runs),
@@ -198,6 +229,7 @@ class DeviceBatch:
             self.regret = torch.zeros(max(B, 1), dtype=torch.float64, device=self.device)
             self.cum = torch.zeros_like(self.regret)
             self.comp = torch.zeros_like(self.regret)
+        self.cum_exact = None  # allocated by ftrl_vs_exact
 
     @property
     def _sp(self):
@@ -280,6 +312,24 @@ class DeviceBatch:
                   self.cum.data_ptr(), self.comp.data_ptr(),
                   cmp_action.data_ptr() if cmp_action is not None else None,
                   regime.data_ptr(), self._sp)
+        return regime
+
+    def ftrl_vs_exact(self, eta0: float = SQRT2, comp_ftl=None, cmp_action=None, regime=None):
+        """ftrl_vs_exact_batch on the resident batch: self.cum gets FTRL's cumulative loss,
+        self.comp the exact comparator's loss, self.cum_exact exact FTL's (allocated on first
+        use); ``comp_ftl`` [B] (device, optional) the loss of FTL(theta_ftrl).  Returns the
+        regime flags."""
+        torch = self.torch
+        n = max(self.L.B, 1)
+        if self.cum_exact is None:
+            self.cum_exact = torch.zeros(n, dtype=torch.float64, device=self.device)
+        if regime is None:
+            regime = torch.zeros(n, dtype=torch.int32, device=self.device)
+        _lib.call("ocx_dev_ftrl_vs_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+                  float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
+                  self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
+                  cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
+                  self._sp)
         return regime
 
     def max_regret(self, out=None):

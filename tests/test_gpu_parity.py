@@ -361,6 +361,37 @@ def test_ftl_exact_matches_oracle(ocx):
         ef.run_ftl_exact(2.0 * z[0], y[0])
 
 
+@pytest.mark.parametrize("B,T,d", [(21, 300, 7), (33, 257, 64), (5, 40, 1024), (4, 0, 3),
+                                   (9, 100, 1)])
+def test_ftrl_vs_exact_fused_matches_oracle(ocx, B, T, d):
+    """One-pass FTRL + exact FTL (ocx_ftrl_vs_exact_batch) == the oracle's closed form and
+    its FTRL run against that comparator; comp_ftl == FTRL's own FTL comparator loss."""
+    eng = ocx["engine"]
+    rng = np.random.default_rng(17 + d)
+    z = rng.standard_normal((B, T, d))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    for P in (1, -1, 4):
+        if P != 1 and d > 64 * abs(P):
+            continue
+        r = eng.ftrl_vs_exact_batch(z, y, SQ2, lanes_per_seq=P, with_ftl_comparator=True)
+        assert r["in_regime"].all()
+        for b in range(B):
+            rc, rp, ra, _ = O.ftl_exact_closed_form(z[b], y[b])
+            fr = O.simulate_alg_full(z[b], y[b], 0, SQ2, comparator=ra)
+            ff = O.simulate_alg_full(z[b], y[b], 0, SQ2)
+            got = [r["cum_exact"][b], r["comp"][b], r["cum_ftrl"][b], r["ftrl"][b],
+                   r["comp_ftl"][b]]
+            want = [rc, rp, fr[1], fr[0], ff[2]]
+            if P != 4:
+                assert got == want and np.array_equal(r["action"][b], ra), (P, b)
+            else:
+                assert close(got, want) and close(r["action"][b], ra), (P, b)
+    if B and T:
+        with pytest.raises(NotImplementedError):
+            eng.ftrl_vs_exact_batch(2.0 * z, y, SQ2)
+
+
 def test_exact_driver_matches_oracle(ocx):
     from online_convex_optimization_amd import drivers
     runs, reps, T = 2, 3, 120

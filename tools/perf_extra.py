@@ -85,31 +85,52 @@ def driver(args):
 
 def config3(args):
     """configs[2]: exact_ftl vs fast FTRL, d=64, T=1e4, 1e5 trials on one GPU: per trial
-    FTRL's regret against the exact comparator and against its own FTL comparator,
-    generation included (resident batches of 32768)."""
+    FTRL's regret against the exact comparator and against its own FTL comparator, and
+    exact FTL's regret, generation included (resident batches of 32768).  Two variants:
+    "fused" (ocx_dev_ftrl_vs_exact: both loops in one pass, comparators in a second) and
+    "separate" (exact FTL kernel, then FTRL twice); their regrets must agree bit for bit."""
     import torch
     from online_convex_optimization_amd import engine
     T, d, trials, Bb = 10000, 64, 100000, 32768
-    t0 = time.perf_counter()
-    diffs = []
-    for r0 in range(0, trials, Bb):
-        B = min(Bb, trials - r0)
-        db = engine.DeviceBatch(B, T, d, lanes_per_seq=1)
-        db.generate_gT(0, r0)
-        act = torch.zeros((B, d), dtype=torch.float64, device=db.device)
-        regime = db.ftl_exact(cmp_action=act)
-        exact = db.simulate_alg(0, math.sqrt(2), comparator=act).clone()
-        fast = db.simulate_alg(0, math.sqrt(2)).clone()
-        assert bool(regime[:B].all())
-        diffs.append((exact[:B] - fast[:B]).cpu().numpy())
-        del db
-    sync()
-    dt = time.perf_counter() - t0
-    dd = np.concatenate(diffs)
-    print(json.dumps({"what": "config3_exact_vs_fast", "trials": trials, "T": T, "d": d,
-                      "seconds": dt, "trial_steps_per_s": trials * T / dt,
-                      "mean_regret_exact_minus_fast": float(dd.mean()),
-                      "max_abs_diff": float(np.abs(dd).max())}), flush=True)
+    db = engine.DeviceBatch(Bb, T, d, lanes_per_seq=1)
+    results = {}
+    for variant in ("fused", "separate", "fused"):
+        sync()
+        t0 = time.perf_counter()
+        out = []
+        for r0 in range(0, trials, Bb):
+            B = min(Bb, trials - r0)
+            if B != db.L.B:
+                del db
+                db = engine.DeviceBatch(B, T, d, lanes_per_seq=1)
+            db.generate_gT(0, r0)
+            if variant == "fused":
+                cf = torch.zeros(B, dtype=torch.float64, device=db.device)
+                regime = db.ftrl_vs_exact(math.sqrt(2), comp_ftl=cf)
+                exact = db.cum - db.comp
+                fast = db.cum - cf
+                ftl_exact = db.cum_exact - db.comp
+            else:
+                act = torch.zeros((B, d), dtype=torch.float64, device=db.device)
+                regime = db.ftl_exact(cmp_action=act)
+                ftl_exact = (db.cum - db.comp).clone()
+                exact = db.simulate_alg(0, math.sqrt(2), comparator=act).clone()
+                fast = db.simulate_alg(0, math.sqrt(2)).clone()
+            assert bool(regime[:B].all())
+            out.append(torch.stack([exact[:B], fast[:B], ftl_exact[:B]]).cpu().numpy())
+        sync()
+        dt = time.perf_counter() - t0
+        res = np.concatenate(out, axis=1)
+        results[variant] = res
+        dd = res[0] - res[1]
+        print(json.dumps({"what": "config3_exact_vs_fast", "variant": variant, "trials": trials,
+                          "T": T, "d": d, "seconds": dt, "trial_steps_per_s": trials * T / dt,
+                          "mean_regret_exact_minus_fast": float(dd.mean()),
+                          "max_abs_diff": float(np.abs(dd).max()),
+                          "mean_regret_ftl_exact": float(res[2].mean())}), flush=True)
+    print(json.dumps({"what": "config3_fused_equals_separate",
+                      "bitexact": bool(np.array_equal(results["fused"], results["separate"]))}),
+          flush=True)
 
 
 def exact_driver(args):
