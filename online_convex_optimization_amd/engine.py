@@ -9,6 +9,10 @@ Two ways in:
   layout (``include/ocx.h``), generated on device or packed once, then simulated
   any number of times without touching the host.  Device memory and streams come
   from PyTorch (plumbing only); every kernel is the HIP code in ``csrc/``.
+
+Every call defaults to ``lanes_per_seq=1`` (exact mode: the reference's sequential sums,
+bit-identical results).  ``lanes_per_seq=0`` selects the butterfly layout, faster only
+where exact chains are latency-bound (d in the hundreds and up; ~1e-16 relative).
 """
 from __future__ import annotations
 
@@ -38,7 +42,7 @@ def _check_zy(z: np.ndarray, y: np.ndarray):
 
 
 def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=None, *,
-                       lanes_per_seq: int = 0, device: int = 0, return_all: bool = False):
+                       lanes_per_seq: int = 1, device: int = 0, return_all: bool = False):
     """fast_algorithms.py:88-115 over B independent sequences on one GPU.
 
     z [B, T, d], y [B, T]; comparator [B, d] optional (exact_ftl.py:266-269).
@@ -62,7 +66,7 @@ def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=
     return reg
 
 
-def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = 0,
+def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = 1,
                          device: int = 0, return_switch: bool = False):
     """fast_algorithms.py:118-164 over B sequences; thresh scalar or [B]."""
     z = _f64(z)
@@ -156,7 +160,7 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, de
 
 
 def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
-               run0: int = 0, lanes_per_seq: int = 0, device: int = 0) -> np.ndarray:
+               run0: int = 0, lanes_per_seq: int = 1, device: int = 0) -> np.ndarray:
     """Regrets of FTRL on _rng(base_seed, T, run) sequences, run in [run0, run0+runs),
     generated on device (fast_algorithms.py:230-241 with a ``d`` parameter)."""
     if base_seed < 0 or base_seed >= 2 ** 64:
@@ -176,7 +180,7 @@ def max_regret(regrets: np.ndarray) -> float:
 
 def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
              eta0: float = SQRT2, devices: Optional[Sequence[int]] = None,
-             lanes_per_seq: int = 0) -> dict:
+             lanes_per_seq: int = 1) -> dict:
     """empirical_worst_case_thresholds on one or several GPUs of this process.
 
     Runs are split into contiguous shards, one per device, each generated and
@@ -216,7 +220,7 @@ class DeviceBatch:
     of this object is launched on it, so torch events recorded on that stream
     bracket the HIP kernels exactly."""
 
-    def __init__(self, B: int, T: int, d: int, *, lanes_per_seq: int = 0, device: int = 0,
+    def __init__(self, B: int, T: int, d: int, *, lanes_per_seq: int = 1, device: int = 0,
                  stream=None):
         import torch
         self.torch = torch
