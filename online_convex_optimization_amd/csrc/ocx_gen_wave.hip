@@ -311,7 +311,7 @@ constexpr int kWaveBlock = 256;
 // (80 VGPRs, a few cold spills) measured 6 % faster than the unconstrained 104 VGPRs
 // (4 waves); its LDS (6 KB tables + 4 x 4 KB rings per block) also admits 6.
 #ifndef OCX_GENW_MIN_WAVES
-#define OCX_GENW_MIN_WAVES_FOR(DF) ((DF) == 64 ? 6 : 1)
+#define OCX_GENW_MIN_WAVES_FOR(DF) ((DF) == 64 ? 6 : ((DF) == 1024 ? 4 : 1))
 #else
 #define OCX_GENW_MIN_WAVES_FOR(DF) OCX_GENW_MIN_WAVES
 #endif
@@ -333,7 +333,11 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 // MODE 1 (seek): st_out[b] = the fresh stream, lab_out[b] = the stream after its
 //   T_seed·d normals, i.e. where choice(T) starts.
 // DF = 64: the d = 64, P·C = 64 rows of every configs[] workload, with the row shape
-// known at compile time; DF = 0: any d.
+// known at compile time; DF = 1024: configs[4]'s d = 1024 rows (P·C = 1024, any P):
+// the ring holds exactly one row (rounds stop at the row's end), the pairwise sum of
+// squares uses all 64 lanes (8 leaves of 128, 8 accumulators each: the leaf and tree
+// order of NumPy's recursion is the 64-lane butterfly) and every store instruction
+// writes whole contiguous plane segments; DF = 0: any d.
 template <int MODE, int DF>
 __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
@@ -370,7 +374,12 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
     }
     const int d = DF ? DF : d_arg;
     const int S = 64 / P;
-    const int Dp = DF ? 64 : P * C;
+    constexpr bool W1K = (DF == 1024);
+    const int Dp = DF == 64 ? 64 : P * C;
+    // DF = 1024 store map: flat index f = i*64 + lane of the row → plane k = f / (2P),
+    // offset w = f % (2P) of the sequence's segment in that plane, coordinate
+    // j = (w/2)*C + 2k + (w%2)
+    const int lg2P = __builtin_ctz((unsigned)(2 * P));
     // rows leave the ring in batches of R: the sums of squares of a batch run side by
     // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
     const int R = batch_rows(d);
@@ -415,7 +424,8 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
         int ready = 0;                 // whole rows waiting in the ring
         int64_t t = 0;
         while (remaining > 0) {
-            const int need = remaining < 64 ? (int)remaining : 64;
+            int need = remaining < 64 ? (int)remaining : 64;
+            if (W1K && MODE == 0 && need > d - (int)partial) need = d - (int)partial;
             const int n = zig_round<MODE == 0>(w, need, tb, ring, rmask, head, lane);
             head += n;
             remaining -= (uint32_t)n;
@@ -424,6 +434,33 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
             while (partial >= (unsigned)d) {
                 partial -= (unsigned)d;
                 ++ready;
+            }
+            if constexpr (W1K && MODE == 0) {
+                if (ready) {  // one whole row in the ring, starting at tailp
+                    const unsigned o = tailp + (unsigned)((lane >> 3) * 128 + (lane & 7));
+                    double v[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) v[q] = ring[(o + 8u * q) & rmask];
+                    double acc = v[0] * v[0];
+#pragma unroll
+                    for (int q = 1; q < 16; ++q) acc += v[q] * v[q];
+                    const double nrm = sqrt(ocx_seq_sum<64>(acc));
+                    const double scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
+                    double* zrow = zt + (int64_t)g * T * 128 + t * 128 + (int64_t)s * 2 * P;
+                    const int64_t kst = G * T * 128;
+#pragma unroll 4
+                    for (int i = 0; i < 16; ++i) {
+                        const int f = i * 64 + lane;
+                        const int k = f >> lg2P, w = f & (2 * P - 1);
+                        const int j = (w >> 1) * C + 2 * k + (w & 1);
+                        __builtin_nontemporal_store(ring[(tailp + (unsigned)j) & rmask] * scr,
+                                                    zrow + k * kst + w);
+                    }
+                    tailp += (unsigned)d;
+                    ++t;
+                    ready = 0;
+                }
+                continue;
             }
             while (ready >= R || (remaining == 0 && ready > 0)) {
                 const int nrows = ready < R ? ready : R;
@@ -531,7 +568,8 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
 
 namespace {
 
-int ring_doubles(int64_t d) {
+int ring_doubles(int64_t d, int DF) {
+    if (DF == 1024) return 1024;  // exactly one row: rounds stop at the row's end
     // a full batch of rows plus one round of normals
     int rb = 128;
     while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
@@ -543,7 +581,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
                           int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
                           double* ytl, const uint64_t* st_in, uint64_t* st_out,
                           const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
-    const int rb = (MODE == 0) ? ring_doubles(d) : 0;
+    const int rb = (MODE == 0) ? ring_doubles(d, DF) : 0;
     const size_t lds =
         (MODE == 0) ? (size_t)(rb + (d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
     // resident waves: fill the GPU once, sequences spread evenly over the waves
@@ -575,6 +613,9 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
     if (d == 64 && (MODE == 1 || (int64_t)P * C == 64))
         return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
                                         st_in, st_out, lab_in, lab_out, st);
+    if (MODE == 0 && d == 1024 && (int64_t)P * C == 1024 && P <= 64)
+        return launch_wave_df<MODE, 1024>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt,
+                                          ytl, st_in, st_out, lab_in, lab_out, st);
     return launch_wave_df<MODE, 0>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
                                    st_in, st_out, lab_in, lab_out, st);
 }

@@ -136,7 +136,8 @@ def test_published_gT_curve(ocx):
 # ------------------------------------------------------------------ generator
 @pytest.mark.parametrize("B,T,d,P", [(70, 50, 5, 1), (33, 20, 64, 4), (5, 8, 1024, 64),
                                      (40, 9, 129, 0), (3, 11, 2, 0), (9, 6, 64, -1),
-                                     (17, 7, 100, -2), (192, 2000, 64, 1)])
+                                     (17, 7, 100, -2), (192, 2000, 64, 1), (6, 40, 1024, 1),
+                                     (4, 10, 1024, 0), (3, 5, 1024, -16), (70, 3, 1024, -32)])
 def test_device_generator_matches_numpy(ocx, B, T, d, P):
     import torch
     eng = ocx["engine"]

@@ -133,6 +133,42 @@ def config3(args):
           flush=True)
 
 
+def config4(args):
+    """configs[4]: g(T) adversary at d=1024, T=1e4 (runs scaled down), generation included,
+    exact and butterfly sums, at two HBM budgets (resident vs streamed batches)."""
+    from online_convex_optimization_amd import engine
+    T, d = 10000, 1024
+    for runs, lanes, budget in ((8192, 1, "64"), (8192, 0, "64"), (8192, 1, "200"),
+                                (8192, 0, "200"), (32768, 0, "200")):
+        os.environ["OCX_HBM_BUDGET_GB"] = budget
+        engine.gT_regrets(T, 256, d=d, lanes_per_seq=lanes)  # warm
+        t0 = time.perf_counter()
+        regs = engine.gT_regrets(T, runs, d=d, lanes_per_seq=lanes)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"what": "config4_gT", "T": T, "runs": runs, "d": d, "lanes": lanes,
+                          "hbm_budget_gb": budget, "seconds": dt,
+                          "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
+              flush=True)
+    os.environ.pop("OCX_HBM_BUDGET_GB", None)
+
+
+def sweep_budget(args):
+    """configs[3] points at the default and a 200 GiB HBM budget (resident batch size)."""
+    from online_convex_optimization_amd import engine
+    for T, runs in ((10000, 131072), (100000, 32768)):
+        for budget in ("64", "200"):
+            os.environ["OCX_HBM_BUDGET_GB"] = budget
+            engine.gT_regrets(T, 1024, d=64, lanes_per_seq=1)
+            t0 = time.perf_counter()
+            regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
+            dt = time.perf_counter() - t0
+            print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64,
+                              "hbm_budget_gb": budget, "seconds": dt,
+                              "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
+                  flush=True)
+    os.environ.pop("OCX_HBM_BUDGET_GB", None)
+
+
 def exact_driver(args):
     from online_convex_optimization_amd import drivers
     t0 = time.perf_counter()
@@ -174,7 +210,7 @@ def smart(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver"])
+    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget"])
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
