@@ -124,9 +124,11 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     // lane to lane (chain = 1).
     const bool exact = (lanes_per_seq == 1 || lanes_per_seq < 0);
     int P = lanes_per_seq < 0 ? -lanes_per_seq : lanes_per_seq;
-    // fewest lanes with <= 64 coordinates each; most lanes keeping >= 2 coordinates
+    // auto: fewest lanes with <= 16 coordinates each (more coordinates per lane cost
+    // registers, hence occupancy: d = 1024 measured 7.5e7 g(T) timesteps/s at 64 or 32
+    // lanes and 4.7e7 at 16 x 64); most lanes keeping >= 2 coordinates
     int64_t p_min = 1;
-    while (p_min < 64 && ceil_div(d, p_min) > 64) p_min *= 2;
+    while (p_min < 64 && ceil_div(d, p_min) > 16) p_min *= 2;
     int64_t p_max = 1;
     while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
     if (lanes_per_seq == 0) {
@@ -487,11 +489,24 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);
     hipStream_t st = cx->stream;
-    // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB, default 64 GiB)
-    int64_t budget = (int64_t)64 << 30;
-    if (const char* e = std::getenv("OCX_HBM_BUDGET_GB")) budget = (int64_t)(std::atof(e) * (1 << 30));
+    // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB): by default 70 % of
+    // what is free plus what this context already holds, at most 192 GiB
+    int64_t budget;
+    if (const char* e = std::getenv("OCX_HBM_BUDGET_GB")) {
+        budget = (int64_t)(std::atof(e) * (1 << 30));
+    } else {
+        size_t fr = 0, tot = 0;
+        OCX_HIP(hipMemGetInfo(&fr, &tot));
+        const double avail = (double)fr + (double)cx->zt.cap + (double)cx->yt.cap;
+        budget = std::min<int64_t>((int64_t)192 << 30, (int64_t)(0.7 * avail));
+    }
     const int64_t kBatch = 131072;   // streams per batch of the streamed path
-    const int64_t kMinResident = 8192;  // a resident batch must fill the generator and the FTRL kernel
+    // Resident batches (one generation pass) win over the streamed path (seek + two
+    // generation passes) from ~1024 sequences per batch on (OCX_MIN_RESIDENT): d = 1024,
+    // T = 1e4 measured 1.1e8 timesteps/s resident at 2600 per batch vs 7.5e7 streamed;
+    // d = 64, T = 1e5: 1.37e9 resident at 4100 per batch vs 1.13e9 streamed.
+    int64_t kMinResident = 1024;
+    if (const char* e = std::getenv("OCX_MIN_RESIDENT")) kMinResident = std::max<int64_t>(1, std::atoll(e));
     ocx_layout L1;
     if (int rc = ocx_layout_init(std::min<int64_t>(R, kBatch), std::max<int64_t>(T, 1), d,
                                  lanes_per_seq, &L1))
@@ -505,6 +520,8 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     if (!streamed) {
         // whole horizon resident: as many runs per batch as the budget holds
         int64_t chunk = std::max<int64_t>(64, std::min<int64_t>(budget / per_seq, R));
+        const int64_t nbat = (R + chunk - 1) / chunk;
+        chunk = (R + nbat - 1) / nbat;  // equal batches: no small, under-filled last one
         OCX_HIP(cx->out.ensure((size_t)chunk * 8));
         for (int64_t r0 = 0; r0 < R; r0 += chunk) {
             const int64_t nb = std::min(chunk, R - r0);

@@ -138,35 +138,51 @@ def config4(args):
     exact and butterfly sums, at two HBM budgets (resident vs streamed batches)."""
     from online_convex_optimization_amd import engine
     T, d = 10000, 1024
-    for runs, lanes, budget in ((8192, 1, "64"), (8192, 0, "64"), (8192, 1, "200"),
-                                (8192, 0, "200"), (32768, 0, "200")):
-        os.environ["OCX_HBM_BUDGET_GB"] = budget
-        engine.gT_regrets(T, 256, d=d, lanes_per_seq=lanes)  # warm
+    cases = [(8192, 0, None, None), (8192, 1, None, None), (32768, 0, None, None),
+             (8192, 0, "64", "8192"), (8192, 1, "64", "8192")]
+    for runs, lanes, budget, minres in cases:
+        if budget:
+            os.environ["OCX_HBM_BUDGET_GB"] = budget
+        else:
+            os.environ.pop("OCX_HBM_BUDGET_GB", None)
+        if minres:
+            os.environ["OCX_MIN_RESIDENT"] = minres
+        else:
+            os.environ.pop("OCX_MIN_RESIDENT", None)
+        # warm with the same shape: the first call grows the HBM buffers and loads kernels
+        engine.gT_regrets(T, runs, d=d, lanes_per_seq=lanes)
         t0 = time.perf_counter()
         regs = engine.gT_regrets(T, runs, d=d, lanes_per_seq=lanes)
         dt = time.perf_counter() - t0
         print(json.dumps({"what": "config4_gT", "T": T, "runs": runs, "d": d, "lanes": lanes,
-                          "hbm_budget_gb": budget, "seconds": dt,
+                          "hbm_budget_gb": budget, "min_resident": minres, "seconds": dt,
                           "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
               flush=True)
     os.environ.pop("OCX_HBM_BUDGET_GB", None)
+    os.environ.pop("OCX_MIN_RESIDENT", None)
 
 
 def sweep_budget(args):
     """configs[3] points at the default and a 200 GiB HBM budget (resident batch size)."""
     from online_convex_optimization_amd import engine
-    for T, runs in ((10000, 131072), (100000, 32768)):
-        for budget in ("64", "200"):
+    for T, runs, budget, minres in ((10000, 131072, "64", None), (10000, 131072, "200", None),
+                                    (100000, 32768, "64", None), (100000, 32768, "200", "2048")):
+        if True:
             os.environ["OCX_HBM_BUDGET_GB"] = budget
-            engine.gT_regrets(T, 1024, d=64, lanes_per_seq=1)
+            if minres:
+                os.environ["OCX_MIN_RESIDENT"] = minres
+            else:
+                os.environ.pop("OCX_MIN_RESIDENT", None)
+            engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
             t0 = time.perf_counter()
             regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
             dt = time.perf_counter() - t0
             print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64,
-                              "hbm_budget_gb": budget, "seconds": dt,
+                              "hbm_budget_gb": budget, "min_resident": minres, "seconds": dt,
                               "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
                   flush=True)
     os.environ.pop("OCX_HBM_BUDGET_GB", None)
+    os.environ.pop("OCX_MIN_RESIDENT", None)
 
 
 def exact_driver(args):
