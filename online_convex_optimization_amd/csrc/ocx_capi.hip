@@ -146,6 +146,10 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
         int64_t p = 1;
         while (p < 64 && ceil_div(d, p) > cmax) p *= 2;
         while (p < 4 && p * B < 65536 && ceil_div(d, 2 * p) >= 2) p *= 2;
+        // few-wave batches (capacity-limited, e.g. the resident g(T) batch at T = 1e5) are
+        // latency-bound: 8 lanes keeping >= 8 coordinates each (d = 64, T = 1e5, 3328
+        // sequences measured 137 ms at 8 lanes, 172 ms at 4, 146 ms at 16)
+        while (p < 8 && p * B < 32768 && ceil_div(d, 2 * p) >= 8) p *= 2;
         P = (int)p;
     }
     if (P < 1 || P > 64 || (P & (P - 1)) != 0)

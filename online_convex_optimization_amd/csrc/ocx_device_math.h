@@ -18,6 +18,13 @@
 #ifndef OCX_LOAD_NT
 #define OCX_LOAD_NT 1
 #endif
+// Chained (exact) sums with at least this many lanes per sequence form the FTRL step's
+// products with full-lane instructions before the lane chain, and sum the comparator
+// pass two steps at a time (ocx_comp_pass2): in a long chain one lane per group is
+// active, so each instruction moved out of it or paired saves a whole wave issue.
+#ifndef OCX_CHAIN_WIDE_P
+#define OCX_CHAIN_WIDE_P 8
+#endif
 
 constexpr int nb_for(int C) { return C <= 8 ? OCX_NB_LE8 : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32); }
 
@@ -169,6 +176,31 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
         }
         nsq = ocx_seq_sum<P>(a);
         q = ocx_seq_sum<P>(b);
+    } else if constexpr (P >= OCX_CHAIN_WIDE_P) {
+        // long chain: products by every lane at once, only the adds inside the chain
+        const int c = lane % P;
+        double pa[C], pb[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            pa[j] = x[j] * x[j];
+            pb[j] = ocx_zj(z, j) * x[j];
+        }
+        double a = 0.0, b = 0.0;
+        for (int cc = 0; cc < P; ++cc) {
+            if (c == cc) {
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    a += pa[j];
+                    b += pb[j];
+                }
+            }
+            if (cc + 1 < P) {
+                a = ocx_dpp<0x138>(a);
+                b = ocx_dpp<0x138>(b);
+            }
+        }
+        nsq = __shfl(a, lane - c + P - 1, 64);
+        q = __shfl(b, lane - c + P - 1, 64);
     } else {
         const int c = lane % P;
         double a = 0.0, b = 0.0;
@@ -195,6 +227,57 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
         q = ocx_zdot<C, P, CHAIN>(z, x, lane);
     }
     return q;
+}
+
+// Comparator loss Σ_t ½|z_t·xs − y_t| over steps [0, T) of one tile region, added to
+// `comp` in step order (fast_algorithms.py:69-76).  The steps' dot products are
+// independent, so two are summed side by side (ocx_total2): in a long lane chain the
+// second chain fills the issue slots the first one leaves idle.  NBC steps in flight:
+// the pair in use and NBC-2 prefetched.
+template <int C, int P, bool CHAIN, int NBC>
+__device__ __forceinline__ double ocx_comp_pass2(const ocx_d2* __restrict__ zp,
+                                                 const double* __restrict__ yp, int64_t T,
+                                                 int64_t kst, int S, const double (&xs)[C],
+                                                 double comp, int lane) {
+    static_assert(NBC >= 4 && NBC % 2 == 0, "a pair in use and at least a pair in flight");
+    constexpr int K = C / 2;
+    constexpr int64_t tstride = 64;  // ocx_d2 per step within a plane
+    ocx_d2 zb[NBC][K];
+    double yb[NBC];
+#pragma unroll
+    for (int u = 0; u < NBC - 2; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+            yb[u] = yp[u * S];
+        }
+    for (int64_t t0 = 0; t0 < T; t0 += NBC) {
+#pragma unroll
+        for (int u = 0; u < NBC; u += 2) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const int64_t tp = t + NBC - 2 + v;
+                    if (tp < T) {
+                        ocx_load_tile<C>(zb[(u + NBC - 2 + v) % NBC], zp + tp * tstride, kst);
+                        yb[(u + NBC - 2 + v) % NBC] = yp[tp * S];
+                    }
+                }
+                const bool two = t + 1 < T;
+                double p0[C], p1[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    p0[j] = ocx_zj(zb[u], j) * xs[j];
+                    p1[j] = two ? ocx_zj(zb[u + 1], j) * xs[j] : 0.0;
+                }
+                double q0, q1;
+                ocx_total2<C, P, CHAIN>(p0, p1, q0, q1, lane);
+                comp += 0.5 * fabs(q0 - yb[u]);
+                if (two) comp += 0.5 * fabs(q1 - yb[u + 1]);
+            }
+        }
+    }
+    return comp;
 }
 
 

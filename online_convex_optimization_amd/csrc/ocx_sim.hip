@@ -136,25 +136,29 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     }
 
     // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
-#pragma unroll
-    for (int u = 0; u < NB - 1; ++u)
-        if (u < T) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
-            yb[u] = yp[u * S];
-        }
     double comp = 0.0;
-    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+        comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, T, kst, S, xs, 0.0, lane);
+    } else {
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int64_t t = t0 + u;
-            if (t < T) {
-                const int64_t tp = t + NB - 1;
-                if (tp < T) {
-                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                    yb[(u + NB - 1) % NB] = yp[tp * S];
+        for (int u = 0; u < NB - 1; ++u)
+            if (u < T) {
+                ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+                yb[u] = yp[u * S];
+            }
+        for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int64_t t = t0 + u;
+                if (t < T) {
+                    const int64_t tp = t + NB - 1;
+                    if (tp < T) {
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                        yb[(u + NB - 1) % NB] = yp[tp * S];
+                    }
+                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                    comp += 0.5 * fabs(q - yb[u]);
                 }
-                const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
-                comp += 0.5 * fabs(q - yb[u]);
             }
         }
     }

@@ -88,18 +88,23 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
         double xs[C];
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
         double comp = live ? comp_state[b] : 0.0;
-        for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
+        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+            // pairs of steps (its own ring; the one preloaded above goes unused)
+            comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, Tc, kst, S, xs, comp, lane);
+        } else {
+            for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
 #pragma unroll
-            for (int u = 0; u < NB; ++u) {
-                const int64_t t = u0 + u;
-                if (t < Tc) {
-                    const int64_t tp = t + NB - 1;
-                    if (tp < Tc) {
-                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                        yb[(u + NB - 1) % NB] = yp[tp * S];
+                for (int u = 0; u < NB; ++u) {
+                    const int64_t t = u0 + u;
+                    if (t < Tc) {
+                        const int64_t tp = t + NB - 1;
+                        if (tp < Tc) {
+                            ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                            yb[(u + NB - 1) % NB] = yp[tp * S];
+                        }
+                        const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                        comp += 0.5 * fabs(q - yb[u]);
                     }
-                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
-                    comp += 0.5 * fabs(q - yb[u]);
                 }
             }
         }

@@ -54,7 +54,8 @@ def test_layout(B, T, d, P):
 
 def test_auto_layout_choices():
     assert (_lib.layout(32768, 10, 64).P, _lib.layout(32768, 10, 64).C) == (4, 16)
-    assert _lib.layout(1 << 20, 10, 64).P == 1          # enough sequences: exact mode
+    assert _lib.layout(1 << 20, 10, 64).P == 4          # at most 16 coordinates per lane
+    assert _lib.layout(1 << 20, 10, 16).P == 1          # enough sequences: one lane each
     assert _lib.layout(1, 10, 5).C == 2                 # lanes keep >= 2 coordinates
     assert _lib.layout(8, 10, 4096).C == 64             # d/P <= 64
     with pytest.raises(_lib.OCXError):
@@ -65,7 +66,9 @@ def test_auto_layout_choices():
     assert (ex.P, ex.C, ex.chain) == (32, 16, 1)
     assert _lib.layout(3, 10, 64, -1).chain == 0          # exact, one lane per sequence
     ch = _lib.layout(3, 10, 64, 1)                         # exact, auto lanes: chained
-    assert ch.chain == 1 and ch.P == 4 and ch.C == 16
+    assert ch.chain == 1 and ch.P == 8 and ch.C == 8       # few waves: 8 lanes
+    assert _lib.layout(3, 10, 16, 1).P == 4                # keeps >= 8 coords to go past 4
+    assert _lib.layout(8192, 10, 64, 1).P == 4             # 32768 lanes at 4 lanes
     assert (_lib.layout(65536, 10, 16, 1).P, _lib.layout(65536, 10, 16, 1).chain) == (1, 0)
     assert _lib.layout(32768, 10, 64, 1).P == 4
     assert _lib.layout(5, 10, 1024, 1).P == 32

@@ -185,6 +185,19 @@ def sweep_budget(args):
     os.environ.pop("OCX_MIN_RESIDENT", None)
 
 
+def prof_long(args):
+    """One call each of configs[4] (d=1024, T=1e4, 8192 runs, exact) and a T=1e5, d=64
+    sweep point (16384 runs), for rocprofv3 --kernel-trace --stats."""
+    from online_convex_optimization_amd import engine
+    for T, d, runs in ((10000, 1024, 8192), (100000, 64, 16384)):
+        t0 = time.perf_counter()
+        regs = engine.gT_regrets(T, runs, d=d, lanes_per_seq=1)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"what": "prof_long", "T": T, "d": d, "runs": runs, "seconds": dt,
+                          "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
+              flush=True)
+
+
 def exact_driver(args):
     from online_convex_optimization_amd import drivers
     t0 = time.perf_counter()
@@ -226,7 +239,7 @@ def smart(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget"])
+    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget", "prof_long"])
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
