@@ -19,9 +19,9 @@
 #define OCX_LOAD_NT 1
 #endif
 // Chained (exact) sums with at least this many lanes per sequence form the FTRL step's
-// products with full-lane instructions before the lane chain, and sum the comparator
-// pass two steps at a time (ocx_comp_pass2): in a long chain one lane per group is
-// active, so each instruction moved out of it or paired saves a whole wave issue.
+// products with full-lane instructions before the chain (shorter chains form them
+// inside it, saving registers), and with <= 16 coordinates per lane sum the comparator
+// pass two steps at a time (ocx_comp_pass2): a long chain leaves issue slots idle.
 #ifndef OCX_CHAIN_WIDE_P
 #define OCX_CHAIN_WIDE_P 8
 #endif
@@ -54,6 +54,89 @@ __device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
 //         lane adds its products one by one → exactly the reference's sequential
 //         order over all d coordinates (exact mode, P > 1).
 // ---------------------------------------------------------------------------
+//
+// The chain is a diagonal: every hop, EVERY lane adds its C products to the value it
+// holds and then takes its left neighbour's (DPP wave_shr:1, a VALU move).  Lane c's
+// value is the true running sum at hop c (it received lane c-1's sum of hop c-1; lane 0
+// starts from 0.0), and the group's last lane ends with the total; what the other
+// lanes compute is never read.  No exec-mask changes: the chain is one basic block the
+// scheduler interleaves with independent work, with no DPP-after-exec wait states.
+// Long chains (P >= OCX_CHAIN_WIDE_P) use it, with the DPP/readlane broadcast and the
+// comparator's totals left in the last lane; short chains (the bench's P = 4) keep the
+// exec-masked hop and a bpermute, measured 2-9 % faster there.
+
+// hops unrolled per loop iteration (full unroll up to 256 adds per chain)
+constexpr int ocx_chain_unroll(int P, int C) { return P * C <= 256 ? P : (C >= 32 ? 1 : 2); }
+
+// The group's last lane (c = P-1) holds a chained total: hand it to all P lanes.  DPP
+// within a row for P <= 16 (quad_perm / row_half_mirror / row_mirror), readlane for
+// P >= 32 (one or two sequences per wave).
+template <int P>
+__device__ __forceinline__ double ocx_bcast_last(double v, int lane) {
+    if constexpr (P == 1) {
+        return v;
+    } else if constexpr (P == 2) {
+        return ocx_dpp<0xF5>(v);  // quad_perm [1,1,3,3]
+    } else if constexpr (P == 4) {
+        return ocx_dpp<0xFF>(v);  // quad_perm [3,3,3,3]
+    } else if constexpr (P == 8) {
+        const double s1 = ocx_dpp<0xFF>(v);    // lanes 4-7 of the half-row: lane 7's value
+        const double s2 = ocx_dpp<0x141>(s1);  // half-row mirror: lanes 0-3 <- lanes 7-4
+        return (lane & 4) ? s1 : s2;
+    } else if constexpr (P == 16) {
+        const int r = lane & 15;
+        const double s1 = ocx_dpp<0xFF>(v);    // lanes 12-15: lane 15's value
+        const double s2 = ocx_dpp<0x140>(s1);  // row mirror: lanes 0-3 <- lanes 15-12
+        const double m = r >= 12 ? s1 : s2;    // right in lanes 0-3 and 12-15
+        const double s3 = ocx_dpp<0x141>(m);   // half mirrors: 4-7 <- 3-0, 8-11 <- 15-12
+        return (r < 4 || r >= 12) ? m : s3;
+    } else if constexpr (P == 32) {
+        const double lo = ocx_readlane(v, 31), hi = ocx_readlane(v, 63);
+        return lane < 32 ? lo : hi;
+    } else {
+        return ocx_readlane(v, 63);
+    }
+}
+
+// Chained total of p over the group, valid in the group's LAST lane only.
+template <int C, int P>
+__device__ __forceinline__ double ocx_chain_last(const double (&p)[C]) {
+    double acc = 0.0;
+#pragma unroll ocx_chain_unroll(P, C)
+    for (int cc = 0; cc + 1 < P; ++cc) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc += p[j];
+        acc = ocx_dpp<0x138>(acc);
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc += p[j];
+    return acc;
+}
+
+// Two chained totals side by side, valid in the group's last lane only.
+template <int C, int P>
+__device__ __forceinline__ void ocx_chain2_last(const double (&p)[C], const double (&q)[C],
+                                                double& a, double& b) {
+    double x = 0.0, y = 0.0;
+#pragma unroll ocx_chain_unroll(P, C)
+    for (int cc = 0; cc + 1 < P; ++cc) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            x += p[j];
+            y += q[j];
+        }
+        x = ocx_dpp<0x138>(x);
+        y = ocx_dpp<0x138>(y);
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        x += p[j];
+        y += q[j];
+    }
+    a = x;
+    b = y;
+}
+
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
     if constexpr (!CHAIN || P == 1) {
@@ -61,10 +144,8 @@ __device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
 #pragma unroll
         for (int j = 0; j < C; ++j) acc += p[j];
         return ocx_seq_sum<P>(acc);
-    } else {
-        // the running sum moves one lane up per hop (DPP wave_shr:1, lane i <- lane i-1:
-        // a VALU move, no LDS round trip); the group's last lane then holds the total,
-        // which one bpermute hands to all P lanes
+    } else if constexpr (P < OCX_CHAIN_WIDE_P) {
+        // short chain: the hop's lane adds (exec-masked), one bpermute hands the total out
         const int c = lane % P;
         double acc = 0.0;
         for (int cc = 0; cc < P; ++cc) {
@@ -75,6 +156,28 @@ __device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
             if (cc + 1 < P) acc = ocx_dpp<0x138>(acc);
         }
         return __shfl(acc, lane - c + P - 1, 64);
+    } else {
+        return ocx_bcast_last<P>(ocx_chain_last<C, P>(p), lane);
+    }
+}
+
+// The total where the comparator pass needs it: the group's last lane (chain) or
+// every lane (tree).  A running sum of such values is read with ocx_comp_lane_value.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_total_last(const double (&p)[C], int lane) {
+    if constexpr (!CHAIN || P < OCX_CHAIN_WIDE_P) {
+        return ocx_total<C, P, CHAIN>(p, lane);
+    } else {
+        return ocx_chain_last<C, P>(p);
+    }
+}
+
+template <int P, bool CHAIN>
+__device__ __forceinline__ double ocx_comp_lane_value(double comp, int lane) {
+    if constexpr (!CHAIN || P < OCX_CHAIN_WIDE_P) {
+        return comp;
+    } else {
+        return ocx_bcast_last<P>(comp, lane);
     }
 }
 
@@ -92,7 +195,7 @@ __device__ __forceinline__ void ocx_total2(const double (&p)[C], const double (&
         }
         a = ocx_seq_sum<P>(x);
         b = ocx_seq_sum<P>(y);
-    } else {
+    } else if constexpr (P < OCX_CHAIN_WIDE_P) {
         const int c = lane % P;
         double x = 0.0, y = 0.0;
         for (int cc = 0; cc < P; ++cc) {
@@ -110,6 +213,21 @@ __device__ __forceinline__ void ocx_total2(const double (&p)[C], const double (&
         }
         a = __shfl(x, lane - c + P - 1, 64);
         b = __shfl(y, lane - c + P - 1, 64);
+    } else {
+        ocx_chain2_last<C, P>(p, q, a, b);
+        a = ocx_bcast_last<P>(a, lane);
+        b = ocx_bcast_last<P>(b, lane);
+    }
+}
+
+// ocx_total2 with the totals where ocx_total_last leaves them.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ void ocx_total2_last(const double (&p)[C], const double (&q)[C],
+                                                double& a, double& b, int lane) {
+    if constexpr (!CHAIN || P < OCX_CHAIN_WIDE_P) {
+        ocx_total2<C, P, CHAIN>(p, q, a, b, lane);
+    } else {
+        ocx_chain2_last<C, P>(p, q, a, b);
     }
 }
 
@@ -158,11 +276,49 @@ __device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C]
 // z·(sθ) are summed side by side; when ‖sθ‖² <= 1 the action is sθ itself (the
 // reference's rescale does not happen) and that q is the answer.  Otherwise x is
 // rescaled and q summed again.  Every sum keeps the reference's order.
+//
+// Long chains (ocx_ftrl_q_sc): `sc` = −(η0/√t) comes from the caller, computed a step
+// ahead (off the chain's critical path); products by every lane at once, then the
+// diagonal chain.  Returns q and the rescale factor f (1.0 when none): the action is
+// x_j = (sc·θ_j)·f, bit for bit what the reference holds, formed only where needed.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_ftrl_q_sc(const double (&th)[C], const ocx_d2* z, double sc,
+                                                double& f, int lane) {
+    static_assert(CHAIN && P >= OCX_CHAIN_WIDE_P, "long chains only");
+    double pa[C], pb[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        const double xj = sc * th[j];
+        pa[j] = xj * xj;
+        pb[j] = ocx_zj(z, j) * xj;
+    }
+    double nsq, q;
+    ocx_chain2_last<C, P>(pa, pb, nsq, q);
+    nsq = ocx_bcast_last<P>(nsq, lane);
+    q = ocx_bcast_last<P>(q, lane);
+    f = 1.0;
+    if (nsq > 1.0) {
+        f = 1.0 / sqrt(nsq);
+        double x[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) x[j] = (sc * th[j]) * f;
+        q = ocx_zdot<C, P, CHAIN>(z, x, lane);
+    }
+    return q;
+}
+
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const ocx_d2* z,
                                                    int64_t t1, double eta0, double (&x)[C],
                                                    int lane) {
     const double sc = -(eta0 / sqrt((double)t1));
+    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+        double f;
+        const double q = ocx_ftrl_q_sc<C, P, CHAIN>(th, z, sc, f, lane);
+#pragma unroll
+        for (int j = 0; j < C; ++j) x[j] = (sc * th[j]) * f;
+        return q;
+    }
 #pragma unroll
     for (int j = 0; j < C; ++j) x[j] = sc * th[j];
     // products formed where they are summed: no p[]/pq[] arrays held across the sums
@@ -176,32 +332,8 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
         }
         nsq = ocx_seq_sum<P>(a);
         q = ocx_seq_sum<P>(b);
-    } else if constexpr (P >= OCX_CHAIN_WIDE_P) {
-        // long chain: products by every lane at once, only the adds inside the chain
-        const int c = lane % P;
-        double pa[C], pb[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-            pa[j] = x[j] * x[j];
-            pb[j] = ocx_zj(z, j) * x[j];
-        }
-        double a = 0.0, b = 0.0;
-        for (int cc = 0; cc < P; ++cc) {
-            if (c == cc) {
-#pragma unroll
-                for (int j = 0; j < C; ++j) {
-                    a += pa[j];
-                    b += pb[j];
-                }
-            }
-            if (cc + 1 < P) {
-                a = ocx_dpp<0x138>(a);
-                b = ocx_dpp<0x138>(b);
-            }
-        }
-        nsq = __shfl(a, lane - c + P - 1, 64);
-        q = __shfl(b, lane - c + P - 1, 64);
     } else {
+        // short chain: the hop's lane adds (exec-masked), one bpermute hands the totals out
         const int c = lane % P;
         double a = 0.0, b = 0.0;
         for (int cc = 0; cc < P; ++cc) {
@@ -271,13 +403,13 @@ __device__ __forceinline__ double ocx_comp_pass2(const ocx_d2* __restrict__ zp,
                     p1[j] = two ? ocx_zj(zb[u + 1], j) * xs[j] : 0.0;
                 }
                 double q0, q1;
-                ocx_total2<C, P, CHAIN>(p0, p1, q0, q1, lane);
+                ocx_total2_last<C, P, CHAIN>(p0, p1, q0, q1, lane);
                 comp += 0.5 * fabs(q0 - yb[u]);
                 if (two) comp += 0.5 * fabs(q1 - yb[u + 1]);
             }
         }
     }
-    return comp;
+    return ocx_comp_lane_value<P, CHAIN>(comp, lane);
 }
 
 

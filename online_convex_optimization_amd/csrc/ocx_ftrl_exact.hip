@@ -31,7 +31,7 @@ __device__ __forceinline__ void ocx_totals(F&& prod, double (&out)[N], int lane)
             for (int k = 0; k < N; ++k) acc[k] += prod(j, k);
 #pragma unroll
         for (int k = 0; k < N; ++k) out[k] = ocx_seq_sum<P>(acc[k]);
-    } else {
+    } else if constexpr (P < OCX_CHAIN_WIDE_P) {
         const int c = lane % P;
         for (int cc = 0; cc < P; ++cc) {
             if (c == cc) {
@@ -47,6 +47,21 @@ __device__ __forceinline__ void ocx_totals(F&& prod, double (&out)[N], int lane)
         }
 #pragma unroll
         for (int k = 0; k < N; ++k) out[k] = __shfl(acc[k], lane - c + P - 1, 64);
+    } else {
+        // diagonal chain (ocx_device_math.h): every lane adds, the last lane's is the total
+#pragma unroll ocx_chain_unroll(P, C)
+        for (int cc = 0; cc < P; ++cc) {
+#pragma unroll
+            for (int j = 0; j < C; ++j)
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k] += prod(j, k);
+            if (cc + 1 < P) {
+#pragma unroll
+                for (int k = 0; k < N; ++k) acc[k] = ocx_dpp<0x138>(acc[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < N; ++k) out[k] = ocx_bcast_last<P>(acc[k], lane);
     }
 }
 

@@ -23,6 +23,12 @@ __device__ __forceinline__ double ocx_dpp(double v) {
     return __hiloint2double(hi, lo);
 }
 
+__device__ __forceinline__ double ocx_readlane(double v, int src) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), src);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), src);
+    return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double ocx_swz_xor16(double v) {
     // ds_swizzle bit-mode: and 0x1F, or 0, xor 0x10 (within 32-lane halves)
     int lo = __double2loint(v), hi = __double2hiint(v);

@@ -74,6 +74,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         }
 
     double cum = 0.0;
+    double sc_next = -(eta0 / sqrt(1.0));  // FTRL scale of step t, computed a step ahead
     for (int64_t t0 = 0; t0 < T; t0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
@@ -87,7 +88,16 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 double x[C];
                 double q;  // :105
                 if (!ftl) {
-                    q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t + 1, eta0, x, lane);
+                    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+                        const double sc = sc_next;  // computed a step ahead
+                        sc_next = -(eta0 / sqrt((double)(t + 2)));
+                        double fr;
+                        q = ocx_ftrl_q_sc<C, P, CHAIN>(th, zb[u], sc, fr, lane);
+#pragma unroll
+                        for (int j = 0; j < C; ++j) x[j] = (sc * th[j]) * fr;
+                    } else {
+                        q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t + 1, eta0, x, lane);
+                    }
                 } else {
                     ocx_action_ftl<C, P, CHAIN>(th, x, lane);
                     q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
@@ -137,7 +147,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
 
     // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
     double comp = 0.0;
-    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && C <= 16) {
         comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, T, kst, S, xs, 0.0, lane);
     } else {
 #pragma unroll
@@ -156,11 +166,15 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                         ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                         yb[(u + NB - 1) % NB] = yp[tp * S];
                     }
-                    const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                    double p[C];
+#pragma unroll
+                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
+                    const double q = ocx_total_last<C, P, CHAIN>(p, lane);
                     comp += 0.5 * fabs(q - yb[u]);
                 }
             }
         }
+        comp = ocx_comp_lane_value<P, CHAIN>(comp, lane);
     }
 
     if (c == 0 && b < B) {

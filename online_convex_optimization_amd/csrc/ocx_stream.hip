@@ -53,6 +53,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
     if (mode == 0) {
         const bool ftl = (alg_flag != 0);
         double cum = live ? cum_state[b] : 0.0;
+        double sc_next = -(eta0 / sqrt((double)(t0 + 1)));  // a step ahead
         for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
 #pragma unroll
             for (int u = 0; u < NB; ++u) {
@@ -66,7 +67,14 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                     double x[C];
                     double q;
                     if (!ftl) {
-                        q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t0 + t + 1, eta0, x, lane);
+                        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+                            const double sc = sc_next;
+                            sc_next = -(eta0 / sqrt((double)(t0 + t + 2)));
+                            double fr;
+                            q = ocx_ftrl_q_sc<C, P, CHAIN>(th, zb[u], sc, fr, lane);
+                        } else {
+                            q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t0 + t + 1, eta0, x, lane);
+                        }
                     } else {
                         ocx_action_ftl<C, P, CHAIN>(th, x, lane);
                         q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
         double xs[C];
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
         double comp = live ? comp_state[b] : 0.0;
-        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
+        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && C <= 16) {
             // pairs of steps (its own ring; the one preloaded above goes unused)
             comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, Tc, kst, S, xs, comp, lane);
         } else {
@@ -102,11 +110,15 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                             ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
                             yb[(u + NB - 1) % NB] = yp[tp * S];
                         }
-                        const double q = ocx_zdot<C, P, CHAIN>(zb[u], xs, lane);
+                        double p[C];
+#pragma unroll
+                        for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
+                        const double q = ocx_total_last<C, P, CHAIN>(p, lane);
                         comp += 0.5 * fabs(q - yb[u]);
                     }
                 }
             }
+            comp = ocx_comp_lane_value<P, CHAIN>(comp, lane);
         }
         if (live && c == 0) {
             comp_state[b] = comp;

@@ -169,7 +169,7 @@ def test_batch_all_lane_splits(ocx, T, d):
     for flag, eta0 in ((0, SQ2), (1, SQ2), (0, 0.3)):
         ref = O.simulate_alg_batch(z, y, flag, eta0, nthreads=4)
         refc = O.simulate_alg_batch(z, y, flag, eta0, comparator=cmp, nthreads=4)
-        for P in (1, -1, -2, -4, -16, -64, 2, 4, 8, 16, 32, 64):
+        for P in (1, -1, -2, -4, -8, -16, -32, -64, 2, 4, 8, 16, 32, 64):
             if P != 1 and -(-d // abs(P)) > 64:
                 continue
             reg, cum, comp, xl = eng.simulate_alg_batch(z, y, flag, eta0, lanes_per_seq=P,
@@ -200,7 +200,7 @@ def test_smart_batch_splits(ocx, monkeypatch, kernel, B, T, d):
     th = rng.uniform(-1.0, 6.0, size=B)
     ref, sw = O.simulate_smart_batch(z, y, th, SQ2, nthreads=4)
     assert T == 0 or len(set(sw.tolist())) > 1  # a mix of switch steps
-    for P in (1, -1, -4, 2, 4, 8, 64):
+    for P in (1, -1, -2, -4, -8, -16, 2, 4, 8, 64):
         if d > 64 * abs(P) or (P < -1 and -P > 64):
             continue
         got, gsw = eng.simulate_smart_batch(z, y, th, SQ2, lanes_per_seq=P, return_switch=True)
