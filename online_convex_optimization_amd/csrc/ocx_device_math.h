@@ -7,13 +7,18 @@
 // Register-ring depth (steps in flight per wave) by coordinates per lane; tuned on
 // MI355X with tools/tune.py (the -D overrides build the tuning variants).
 #ifndef OCX_NB_LE8
-#define OCX_NB_LE8 4
+#define OCX_NB_LE8 8
 #endif
 #ifndef OCX_NB_16
 #define OCX_NB_16 3
 #endif
 #ifndef OCX_NB_GE32
 #define OCX_NB_GE32 2
+#endif
+// steps in flight in the paired comparator pass (ocx_comp_pass2) for C <= 8 (4 above):
+// the pair in use and OCX_NB_PASS2 - 2 prefetched
+#ifndef OCX_NB_PASS2
+#define OCX_NB_PASS2 8
 #endif
 #ifndef OCX_LOAD_NT
 #define OCX_LOAD_NT 1
@@ -26,7 +31,12 @@
 #define OCX_CHAIN_WIDE_P 8
 #endif
 
-constexpr int nb_for(int C) { return C <= 8 ? OCX_NB_LE8 : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32); }
+// C <= 8: 8 steps (few-wave exact batches are latency-bound: d=64, T=1e5, 8 lanes
+// measured 126 -> 116 ms with 8 here and in the paired comparator pass), except where
+// the ring would not stay in registers (chains of 32+ lanes, the 4-total fused kernel).
+constexpr int nb_for(int C, int P = 1, bool deep = true) {
+    return C <= 8 ? ((deep && P < 32) ? OCX_NB_LE8 : 4) : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32);
+}
 
 template <int C>
 __device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p,
@@ -65,8 +75,8 @@ __device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
 // comparator's totals left in the last lane; short chains (the bench's P = 4) keep the
 // exec-masked hop and a bpermute, measured 2-9 % faster there.
 
-// hops unrolled per loop iteration (full unroll up to 256 adds per chain)
-constexpr int ocx_chain_unroll(int P, int C) { return P * C <= 256 ? P : (C >= 32 ? 1 : 2); }
+// hops unrolled per loop iteration (full unroll up to 128 adds per chain)
+constexpr int ocx_chain_unroll(int P, int C) { return P * C <= 128 ? P : (C >= 32 ? 1 : 2); }
 
 // The group's last lane (c = P-1) holds a chained total: hand it to all P lanes.  DPP
 // within a row for P <= 16 (quad_perm / row_half_mirror / row_mirror), readlane for

@@ -207,7 +207,7 @@ template <int C, int P, bool CH>
 hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt, double eta0,
                         double* cum_r, double* cum_e, double* comp_e, double* comp_f,
                         double* cmp_out, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C)>),
+    hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C, P, false)>),
                        dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
                        dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e,
                        comp_e, comp_f, cmp_out, regime);

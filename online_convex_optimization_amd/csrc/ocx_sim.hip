@@ -147,8 +147,8 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
 
     // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
     double comp = 0.0;
-    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && C <= 16) {
-        comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, T, kst, S, xs, 0.0, lane);
+    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
+        comp = ocx_comp_pass2<C, P, CHAIN, (C <= 8 ? OCX_NB_PASS2 : 4)>(zp, yp, T, kst, S, xs, 0.0, lane);
     } else {
 #pragma unroll
         for (int u = 0; u < NB - 1; ++u)
@@ -384,7 +384,7 @@ template <int C, int P, bool CH>
 hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int algo,
                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
                          double* xl, double* cmp_out, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C)>), dim3(grid_for(L->G)),
+    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), dim3(grid_for(L->G)),
                        dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, algo, eta0, cmp,
                        reg, cum, comp, xl, cmp_out, regime);
     return hipGetLastError();

@@ -96,9 +96,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
         double xs[C];
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
         double comp = live ? comp_state[b] : 0.0;
-        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && C <= 16) {
+        if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
             // pairs of steps (its own ring; the one preloaded above goes unused)
-            comp = ocx_comp_pass2<C, P, CHAIN, 4>(zp, yp, Tc, kst, S, xs, comp, lane);
+            comp = ocx_comp_pass2<C, P, CHAIN, (C <= 8 ? OCX_NB_PASS2 : 4)>(zp, yp, Tc, kst, S, xs, comp, lane);
         } else {
             for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
 #pragma unroll
@@ -132,7 +132,7 @@ template <int C, int P, bool CH>
 hipError_t launch_chunk_cp(const ocx_layout* L, const double* zt, const double* yt, int64_t t0,
                            int alg_flag, double eta0, int mode, double* th, double* cum,
                            double* comp, double* reg, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_alg_chunk_kernel<C, P, CH, nb_for(C)>),
+    hipLaunchKernelGGL((ocx_alg_chunk_kernel<C, P, CH, nb_for(C, P)>),
                        dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
                        dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode,
                        th, L->Dp, cum, comp, reg);
