@@ -14,3 +14,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "$R/gpurun_out/pmc_$C" -o pmc -- python3 "$R/bench.py" --steps 2 --warmup 0 --cpu-seconds 0 > "$R/gpurun_out/pmc_$C.log" 2>&1 || { echo "pmc $C failed"; tail -20 "$R/gpurun_out/pmc_$C.log"; exit 6; }
 done
 cd "$R" && python tools/pmc_traffic.py --fetch gpurun_out/pmc_FETCH_SIZE --write gpurun_out/pmc_WRITE_SIZE --B 32768 --T 10000 --d 64 --P 4 --out gpurun_out/traffic.json && head -8 gpurun_out/prof_final/r01_kernel_stats.csv | cut -c1-160
+cd "$R" && cp gpurun_out/traffic.json profiles/traffic.json && timeout -k 10 600 python bench.py > gpurun_out/bench_default.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_default.log; exit 7; }
+grep '^{' gpurun_out/bench_default.log > gpurun_out/bench_default.json && cut -c1-300 gpurun_out/bench_default.json
