@@ -18,8 +18,10 @@
 template <int CTRL>
 __device__ __forceinline__ double ocx_dpp(double v) {
     int lo = __double2loint(v), hi = __double2hiint(v);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, false);
+    // old = the value itself: a lane without a source (lane 0 under wave_shr) keeps its
+    // own value, which no caller reads, and the move needs no zeroed destination first
+    lo = __builtin_amdgcn_update_dpp(lo, lo, CTRL, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
 
