@@ -72,6 +72,10 @@ typedef struct ocx_layout {
 int ocx_version(void);
 int ocx_last_error(char* buf, size_t len);
 int ocx_device_count(int* count);
+/* Free the HBM the library caches per device for its host entry points and g(T) sweeps
+ * (grown on demand, kept between calls).  Safe between calls; the next call regrows it.
+ * Use before allocating large device buffers of one's own (engine.DeviceBatch). */
+int ocx_release_buffers(int device);
 /* Fill *out for (B, T, d) and a lanes_per_seq request (0 = auto). */
 int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layout* out);
 

@@ -44,6 +44,7 @@ SIGNATURES = {
     "ocx_version": (c_int, []),
     "ocx_last_error": (c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "ocx_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "ocx_release_buffers": (c_int, [c_int]),
     "ocx_layout_init": (c_int, [c_i64, c_i64, c_i64, c_int, ctypes.POINTER(Layout)]),
     "ocx_simulate_alg_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_int, c_double, c_dp,
                                        c_dp, c_dp, c_dp, c_dp, c_int, c_int]),
@@ -137,6 +138,11 @@ def device_count() -> int:
     n = c_int(0)
     call("ocx_device_count", ctypes.byref(n))
     return int(n.value)
+
+
+def release_buffers(device: int = 0) -> None:
+    """Free the HBM the library caches on `device` between calls (ocx_release_buffers)."""
+    call("ocx_release_buffers", int(device))
 
 
 def layout(B: int, T: int, d: int, lanes_per_seq: int = 0) -> Layout:

@@ -38,6 +38,12 @@ constexpr int kMaxDevices = 64;
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    hipError_t release() {
+        hipError_t e = p ? hipFree(p) : hipSuccess;
+        p = nullptr;
+        cap = 0;
+        return e;
+    }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) {
@@ -111,6 +117,18 @@ int ocx_device_count(int* count) {
         return fail(OCX_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
     }
     *count = n;
+    return OCX_OK;
+}
+
+int ocx_release_buffers(int device) {
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    OCX_HIP(hipStreamSynchronize(cx->stream));
+    for (DevBuf* b : {&cx->zraw, &cx->yraw, &cx->zt, &cx->yt, &cx->at, &cx->araw, &cx->cmp,
+                      &cx->thr, &cx->out, &cx->sw, &cx->rstate, &cx->lstate, &cx->theta,
+                      &cx->acc})
+        OCX_HIP(b->release());
     return OCX_OK;
 }
 

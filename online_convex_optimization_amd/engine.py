@@ -171,6 +171,12 @@ def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float
     return out
 
 
+def release_buffers(device: int = 0) -> None:
+    """Free the HBM the engine caches on `device` for host-array calls and g(T) sweeps
+    (it regrows on the next call): do this before allocating a large DeviceBatch."""
+    _lib.release_buffers(device)
+
+
 def max_regret(regrets: np.ndarray) -> float:
     """fast_algorithms.py:228, :242-243 — max over runs starting from 0.0 (`reg > max`)."""
     r = np.asarray(regrets, dtype=np.float64)

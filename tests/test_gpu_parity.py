@@ -411,3 +411,13 @@ def test_exact_driver_matches_oracle(ocx):
         ftl.append(float(np.mean(fl)))
     assert st["FTRL"][0][0] == float(np.mean(ftrl))
     assert st["FTL (exact)"][0][0] == float(np.mean(ftl))
+
+
+def test_release_buffers_then_regrow(ocx):
+    """ocx_release_buffers frees the cached HBM; the next call regrows it, same results."""
+    eng = ocx["engine"]
+    a = eng.gT_regrets(300, 40, d=64, lanes_per_seq=1)
+    eng.release_buffers()
+    eng.release_buffers()  # idempotent
+    b = eng.gT_regrets(300, 40, d=64, lanes_per_seq=1)
+    assert np.array_equal(a, b)

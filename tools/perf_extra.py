@@ -92,6 +92,7 @@ def config3(args):
     import torch
     from online_convex_optimization_amd import engine
     T, d, trials, Bb = 10000, 64, 100000, 32768
+    engine.release_buffers()  # the sweeps' cached HBM, if run in the same process
     db = engine.DeviceBatch(Bb, T, d, lanes_per_seq=1)
     results = {}
     for variant in ("fused", "separate", "fused"):
