@@ -164,26 +164,26 @@ def config4(args):
 
 
 def sweep_budget(args):
-    """configs[3] points at the default and a 200 GiB HBM budget (resident batch size)."""
+    """HBM budget for resident g(T) batches (OCX_HBM_BUDGET_GB): few-wave, latency-bound
+    batches (T=1e5 at d=64, T=1e4 at d=1024) run faster the more sequences a batch holds."""
     from online_convex_optimization_amd import engine
-    for T, runs, budget, minres in ((10000, 131072, "64", None), (10000, 131072, "200", None),
-                                    (100000, 32768, "64", None), (100000, 32768, "200", "2048")):
-        if True:
-            os.environ["OCX_HBM_BUDGET_GB"] = budget
-            if minres:
-                os.environ["OCX_MIN_RESIDENT"] = minres
-            else:
-                os.environ.pop("OCX_MIN_RESIDENT", None)
-            engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
+    cases = [(100000, 64, 32768, b) for b in ("192", "220", "240", "255")]
+    cases += [(10000, 1024, 8192, b) for b in ("192", "240")]
+    for T, d, runs, budget in cases:
+        os.environ["OCX_HBM_BUDGET_GB"] = budget
+        try:
+            engine.release_buffers()
+            engine.gT_regrets(T, runs, d=d, lanes_per_seq=1)
             t0 = time.perf_counter()
-            regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
+            regs = engine.gT_regrets(T, runs, d=d, lanes_per_seq=1)
             dt = time.perf_counter() - t0
-            print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64,
-                              "hbm_budget_gb": budget, "min_resident": minres, "seconds": dt,
-                              "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
-                  flush=True)
+            out = {"seconds": dt, "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}
+        except Exception as e:  # an over-large budget fails allocation: report it
+            out = {"error": str(e)[:200]}
+        print(json.dumps({"what": "gT_budget", "T": T, "runs": runs, "d": d,
+                          "hbm_budget_gb": budget, **out}), flush=True)
     os.environ.pop("OCX_HBM_BUDGET_GB", None)
-    os.environ.pop("OCX_MIN_RESIDENT", None)
+    engine.release_buffers()
 
 
 def prof_long(args):
