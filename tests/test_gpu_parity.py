@@ -332,6 +332,22 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
             assert chunked[r] == ref
 
 
+@pytest.mark.parametrize("T,d,runs", [(50, 64, 700), (2, 1024, 3000)])
+def test_resident_batching_is_invisible(ocx, monkeypatch, T, d, runs):
+    """Resident g(T) batches of any size (exact mode: lanes chosen per batch size; d=1024,
+    3000 runs: 1500 waves, cut to one-round batches) give the same regrets bit for bit."""
+    eng = ocx["engine"]
+    whole = eng.gT_regrets(T, runs, base_seed=2, d=d, run0=5, lanes_per_seq=1)
+    monkeypatch.setenv("OCX_MIN_RESIDENT", "1")
+    per_seq = T * (8 * d + 8)
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(97 * per_seq / 2**30))  # batches of ~97
+    small = eng.gT_regrets(T, runs, base_seed=2, d=d, run0=5, lanes_per_seq=1)
+    assert np.array_equal(whole, small)
+    for r in (0, runs // 2, runs - 1):
+        z, y = O.gT_sample(2, T, 5 + r, d)
+        assert small[r] == O.simulate_alg(z, y, 0, SQ2)
+
+
 # ------------------------------------------------------------------ exact FTL (closed form)
 def test_ftl_exact_matches_oracle(ocx):
     """exact_ftl run_ftl_exact / run_ftrl(no comparator) on the GPU == the oracle's closed
