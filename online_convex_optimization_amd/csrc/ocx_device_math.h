@@ -282,6 +282,23 @@ __device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C]
     return ocx_total<C, P, CHAIN>(p, lane);
 }
 
+// FTRL scales s_t = −(η0/√t) of 64 consecutive steps, one per lane, refreshed every 64
+// steps (fast_algorithms.py:58): the sqrt/div sequence costs one lane-parallel pass per 64
+// steps instead of one per step, and step t reads its value with a readlane.  The same
+// expression per t as the per-step form, so bit for bit the same scale.
+struct OcxScaleTable {
+    double v = 0.0;
+    int64_t base = INT64_MIN / 2;  // 1-based step of lane 0's entry (none yet)
+};
+__device__ __forceinline__ double ocx_ftrl_scale(OcxScaleTable& tb, int64_t t1, double eta0,
+                                                 int lane) {
+    if (t1 - tb.base >= 64 || t1 < tb.base) {
+        tb.base = t1;
+        tb.v = -(eta0 / sqrt((double)(t1 + lane)));
+    }
+    return ocx_readlane(tb.v, (int)(t1 - tb.base));
+}
+
 // FTRL action and q = z_t·x in one pass (fast_algorithms.py:52-66, :105).  ‖sθ‖² and
 // z·(sθ) are summed side by side; when ‖sθ‖² <= 1 the action is sθ itself (the
 // reference's rescale does not happen) and that q is the answer.  Otherwise x is

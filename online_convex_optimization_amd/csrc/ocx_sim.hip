@@ -74,7 +74,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         }
 
     double cum = 0.0;
-    double sc_next = -(eta0 / sqrt(1.0));  // FTRL scale of step t, computed a step ahead
+    OcxScaleTable sct;  // FTRL scales, 64 steps at a time (long chains)
     for (int64_t t0 = 0; t0 < T; t0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
@@ -89,8 +89,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 double q;  // :105
                 if (!ftl) {
                     if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
-                        const double sc = sc_next;  // computed a step ahead
-                        sc_next = -(eta0 / sqrt((double)(t + 2)));
+                        const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);
                         double fr;
                         q = ocx_ftrl_q_sc<C, P, CHAIN>(th, zb[u], sc, fr, lane);
 #pragma unroll

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
     if (mode == 0) {
         const bool ftl = (alg_flag != 0);
         double cum = live ? cum_state[b] : 0.0;
-        double sc_next = -(eta0 / sqrt((double)(t0 + 1)));  // a step ahead
+        OcxScaleTable sct;  // FTRL scales, 64 steps at a time (long chains)
         for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
 #pragma unroll
             for (int u = 0; u < NB; ++u) {
@@ -68,8 +68,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                     double q;
                     if (!ftl) {
                         if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
-                            const double sc = sc_next;
-                            sc_next = -(eta0 / sqrt((double)(t0 + t + 2)));
+                            const double sc = ocx_ftrl_scale(sct, t0 + t + 1, eta0, lane);
                             double fr;
                             q = ocx_ftrl_q_sc<C, P, CHAIN>(th, zb[u], sc, fr, lane);
                         } else {
