@@ -98,6 +98,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
             yb[u] = yp[u * S];
         }
     double cr = 0.0, ce = 0.0;
+    OcxScaleTable sct;  // FTRL scales, 64 steps at a time
     for (int64_t t0 = 0; t0 < T; t0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
@@ -111,7 +112,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
                 const ocx_d2* z = zb[u];
                 const double yv = yb[u];
                 // FTRL action terms (fast_algorithms.py:52-66), exact-FTL norm, ‖z_t‖²
-                const double sc = -(eta0 / sqrt((double)(t + 1)));
+                const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);
                 double xr[C];
 #pragma unroll
                 for (int j = 0; j < C; ++j) xr[j] = sc * tr[j];
