@@ -146,6 +146,10 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
 
     // ---- second streaming pass: comparator loss (fast_algorithms.py:69-76) ----
     double comp = 0.0;
+#ifdef OCX_TUNE_SKIP_COMP  // tuning only: time the FTRL pass alone (regrets are wrong)
+    if (true) {
+    } else
+#endif
     if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
         comp = ocx_comp_pass2<C, P, CHAIN, (C <= 8 ? OCX_NB_PASS2 : 4)>(zp, yp, T, kst, S, xs, 0.0, lane);
     } else {
