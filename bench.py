@@ -23,6 +23,7 @@ import argparse
 import json
 import math
 import os
+import platform
 import sys
 import time
 
@@ -45,6 +46,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=1,
                     help="lanes_per_seq (include/ocx.h): 1 = exact mode (bit-identical to the "
                          "reference, auto lanes), 0 = auto with butterfly sums, k / -k explicit")
+    ap.add_argument("--e2e-steps", type=int, default=3,
+                    help="untimed-for-the-metric batches of generation + simulation reported "
+                         "as end_to_end (0 disables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="budget of the CPU-baseline sample (0 disables)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -74,11 +78,12 @@ def cpu_baseline(T, d, runs, budget_s):
 
 def cpu_baseline_all_cores(T, d, budget_s):
     """The same C port with one sequence per OpenMP thread on every host core the box
-    gives this process (reported beside the 1-core number; not the target)."""
+    gives this process (reported beside the 1-core number; not the target).  The sample
+    holds 4 sequences per thread so every thread stays busy for the whole call."""
     from oracle import oracle as O
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = max(1, min(int(threads), int(os.environ.get("OMP_NUM_THREADS", threads))))
-    n = max(threads, 2 * threads)
+    n = 4 * threads
     zs, ys = zip(*[O.gT_sample(0, T, r, d) for r in range(n)])
     z = np.stack(zs)
     y = np.stack(ys)
@@ -88,7 +93,23 @@ def cpu_baseline_all_cores(T, d, budget_s):
         O.simulate_alg_batch(z, y, 0, math.sqrt(2), nthreads=threads)
         spent += time.perf_counter() - t0
         steps += n * T
-    return steps / spent, threads, n
+    return steps / spent, threads, n, spent
+
+
+def host_cpu():
+    """CPU model and core counts of the host this bench runs on."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"model": model or platform.processor() or platform.machine(),
+            "nproc": os.cpu_count(), "affinity": aff}
 
 
 def main():
@@ -101,7 +122,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = local % torch.cuda.device_count() if a.dist_backend == "gloo" else local
-    if world > 1:
+    # under torchrun (even with one rank) the process group and the gather are real
+    dist_on = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if dist_on:
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
@@ -119,7 +142,7 @@ def main():
     torch.cuda.synchronize()
     gen_s = time.perf_counter() - tg0
     gdev = dev if a.dist_backend == "nccl" else torch.device("cpu")
-    gathered = torch.zeros(world * B, dtype=torch.float64, device=gdev) if world > 1 else None
+    gathered = torch.zeros(world * B, dtype=torch.float64, device=gdev) if dist_on else None
 
     def gather():
         # the path's one exchange: every rank's regrets to every rank
@@ -128,12 +151,12 @@ def main():
 
     def step():
         db.simulate_alg(0, math.sqrt(2))
-        if world > 1:
+        if dist_on:
             gather()
 
     for _ in range(a.warmup):
         step()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -143,17 +166,49 @@ def main():
         ev[i][0].record(stream)
         db.simulate_alg(0, math.sqrt(2))
         ev[i][1].record(stream)
-        if world > 1:
+        if dist_on:
             gather()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         t = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+    # End to end (outside the metric's timed region): regenerate the batch on device and
+    # simulate it, a.e2e_steps times — what a g(T) sweep / configs[2] job does per batch.
+    e2e = None
+    if a.e2e_steps > 0:
+        eg = [[torch.cuda.Event(enable_timing=True) for _ in range(3)]
+              for _ in range(a.e2e_steps)]
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        te0 = time.perf_counter()
+        for i in range(a.e2e_steps):
+            eg[i][0].record(stream)
+            db.generate_gT(base_seed=0, run0=run0)
+            eg[i][1].record(stream)
+            db.simulate_alg(0, math.sqrt(2))
+            eg[i][2].record(stream)
+        torch.cuda.synchronize()
+        e2e_s = time.perf_counter() - te0
+        if dist_on:
+            t = torch.tensor([e2e_s], dtype=torch.float64, device=gdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e2e_s = float(t.item())
+        gen_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in eg]))
+        sim_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in eg]))
+        rate = world * B * T * a.e2e_steps / e2e_s
+        e2e = {"timesteps_per_s": rate, "steps": a.e2e_steps,
+               "ms_per_batch": e2e_s / a.e2e_steps * 1e3,
+               "gen_kernel_ms": gen_ms, "sim_kernel_ms": sim_ms,
+               "roofline_frac": rate / world * 2 * (8 * d + 8) / (PEAK_HBM_GBS * 1e9),
+               "note": "generation (ocx_dev_gen_gT) + FTRL per resident batch; frac counts the "
+                       "FTRL kernel's 2*(8d+8) B/timestep only"}
 
     regrets = db.regret[:B].cpu().numpy()
     out = None
@@ -178,14 +233,17 @@ def main():
             parity = {"n_checked": int(len(cregs)), "max_abs_err": float(err.max()),
                       "max_rel_err": float((err / np.maximum(np.abs(cregs), 1e-300)).max()),
                       "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs))}
+            acps, threads, nseq, aspent = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 4))
+            hc = host_cpu()
             cpu = {"value": cps, "unit": "timesteps/s", "cores": 1, "kind": "port",
                    "sample": f"{len(cregs)} sequences of the same workload (d={d}, T={T}, "
-                             f"runs 0..{len(cregs) - 1}), oracle/ocx_oracle.c single thread, "
-                             f"{spent:.1f} s"}
-            acps, threads, nseq = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 4))
-            cpu["all_cores"] = {"value": acps, "cores": threads,
-                                "sample": f"{nseq} sequences, one per OpenMP thread, "
-                                          "oracle/ocx_oracle.c"}
+                             f"runs 0..{len(cregs) - 1}), oracle/ocx_oracle.c (gcc -O3 "
+                             f"-ffp-contract=off) single thread, {spent:.1f} s",
+                   "cpu_model": hc["model"], "host_nproc": hc["nproc"],
+                   "host_affinity": hc["affinity"],
+                   "value_all_cores": acps, "cores_all": threads,
+                   "sample_all_cores": f"{nseq} sequences ({nseq // threads} per OpenMP "
+                                       f"thread), runs 0..{nseq - 1}, {aspent:.1f} s"}
         out = {
             "metric": "FTRL timesteps/sec (whole node) at d=64, T=1e4; max |regret-ref| error",
             "value": value,
@@ -214,15 +272,16 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "parity": parity,
+            "end_to_end": e2e,
             "gen_seconds": gen_s,
             "gen_timesteps_per_s": B * T / gen_s,
         }
-        if world > 1:
+        if dist_on:
             g = gathered.cpu().numpy()
             out["gathered_check"] = bool(np.array_equal(g[:B], regrets))
             out["dist_backend"] = a.dist_backend
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
     return out

@@ -110,6 +110,15 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
                         int norm, double* cum_loss, double* comp_loss, double* cmp_action,
                         int32_t* regime, int lanes_per_seq, int device);
 
+/* exact_ftl.py:280-303 compute_prefix_actions (ExactFTLNoClip, norm 0 = l2), batched:
+ * actions [B][T+1][d] row-major, actions[b][t] = the exact FTL solution of prefix length
+ * t, in the closed form of ocx_ftl_exact_batch (S_t/||S_t||, 0 for S_t = 0), with the
+ * same regime flags (int32 [B], required).  Replaying these actions (ocx_replay_batch)
+ * gives ocx_ftl_exact_batch's cum_loss bit for bit.  Parity vs cvxpy: unpinned. */
+int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, int64_t T,
+                                 int64_t d, int norm, double* actions, int32_t* regime,
+                                 int lanes_per_seq, int device);
+
 /* exact_ftl_driver.py:157-186 per sequence, batched, in one read of the data: exact FTL
  * (as ocx_ftl_exact_batch, l2 closed form) and FTRL (fast_algorithms.py:88-111 order,
  * eta0) against the exact comparator actions[T] (exact_ftl.py:399-420 run_ftrl with
@@ -169,6 +178,11 @@ int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const doubl
 int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
                       double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
                       void* stream);
+
+/* ocx_ftl_prefix_actions_batch on device: actions [B][T+1][d] row-major (device). */
+int ocx_dev_ftl_prefix_actions(const ocx_layout* L, const double* z_tiled,
+                               const double* y_tiled, int norm, double* actions,
+                               int32_t* regime, void* stream);
 
 /* ocx_ftrl_vs_exact_batch on device: both loops in one pass, both comparator losses in
  * a second (two HBM passes instead of four). */

@@ -54,6 +54,10 @@ SIGNATURES = {
                                     ctypes.POINTER(ctypes.c_int32), c_int, c_int]),
     "ocx_dev_ftl_exact": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp,
                                   c_vp]),
+    "ocx_ftl_prefix_actions_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_int, c_dp,
+                                             ctypes.POINTER(ctypes.c_int32), c_int, c_int]),
+    "ocx_dev_ftl_prefix_actions": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_vp, c_vp,
+                                           c_vp]),
     "ocx_ftrl_vs_exact_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_double, c_dp, c_dp,
                                         c_dp, c_dp, c_dp, ctypes.POINTER(ctypes.c_int32), c_int,
                                         c_int]),

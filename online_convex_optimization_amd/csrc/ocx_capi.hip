@@ -78,9 +78,15 @@ int ctx_enter(int device, DevCtx** out) {
                                        std::to_string(n) + ")");
     OCX_HIP(hipSetDevice(device));
     DevCtx* c = &g_ctx[device];
-    if (!c->init) {
-        OCX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        c->init = true;
+    {
+        // one stream per device even when threads enter concurrently (gT_sweep over
+        // several devices, or two host calls on one device)
+        static std::mutex init_mu;
+        std::lock_guard<std::mutex> lk(init_mu);
+        if (!c->init) {
+            OCX_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            c->init = true;
+        }
     }
     *out = c;
     return OCX_OK;
@@ -266,6 +272,19 @@ int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* 
     return OCX_OK;
 }
 
+int ocx_dev_ftl_prefix_actions(const ocx_layout* L, const double* z_tiled,
+                               const double* y_tiled, int norm, double* actions,
+                               int32_t* regime, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (L->B && (!regime || (L->d > 0 && !actions)))
+        return fail(OCX_E_INVALID, "NULL output buffer");
+    OCX_HIP(ocx_launch_prefix_actions(L, z_tiled, y_tiled, actions, regime,
+                                      (hipStream_t)stream));
+    return OCX_OK;
+}
+
 int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                           double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                           double* comp_ftl, double* cmp_action, int32_t* regime, void* stream) {
@@ -422,6 +441,39 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
     if (cum_loss) std::memcpy(cum_loss, h.data(), B * 8);
     if (comp_loss) std::memcpy(comp_loss, h.data() + B, B * 8);
     if (cmp_action && d) std::memcpy(cmp_action, h.data() + 2 * B, (size_t)B * d * 8);
+    return OCX_OK;
+}
+
+int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, int64_t T,
+                                 int64_t d, int norm, double* actions, int32_t* regime,
+                                 int lanes_per_seq, int device) {
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || !regime || (d > 0 && !actions))
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T), na = (size_t)(B * (T + 1) * d);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->araw.ensure(na * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * 4));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
+                            cx->yt.as<double>(), st));
+    int* rg = cx->out.as<int>();
+    OCX_HIP(ocx_launch_prefix_actions(&L, cx->zt.as<double>(), cx->yt.as<double>(),
+                                      cx->araw.as<double>(), rg, st));
+    if (na) OCX_HIP(hipMemcpyAsync(actions, cx->araw.p, na * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
     return OCX_OK;
 }
 
@@ -588,10 +640,17 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     const int64_t Bc = L1.B;
     OCX_HIP(cx->rstate.ensure((size_t)(nch + 1) * Bc * 48));
     OCX_HIP(cx->lstate.ensure((size_t)(nch + 1) * Bc * 48));
-    OCX_HIP(cx->theta.ensure((size_t)Bc * L1.Dp * 8));
+    // theta rows are Dp wide, and Dp follows each batch's own layout (the lane rule
+    // depends on the batch size, so a short last batch can have more, narrower lanes):
+    // size for the widest batch and zero each batch with its own Dp
+    ocx_layout Ltail;
+    if (int rc = ocx_layout_init(R % Bc ? R % Bc : Bc, 1, d, lanes_per_seq, &Ltail)) return rc;
+    OCX_HIP(cx->theta.ensure((size_t)std::max(Bc * L1.Dp, Ltail.B * Ltail.Dp) * 8));
     OCX_HIP(cx->acc.ensure((size_t)Bc * 3 * 8));
     for (int64_t r0 = 0; r0 < R; r0 += Bc) {
         const int64_t nb = std::min(Bc, R - r0);
+        ocx_layout Lb;
+        if (int rc = ocx_layout_init(nb, 1, d, lanes_per_seq, &Lb)) return rc;
         uint64_t* rs = cx->rstate.as<uint64_t>();
         uint64_t* ls = cx->lstate.as<uint64_t>();
         double* th = cx->theta.as<double>();
@@ -599,7 +658,7 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
         double* comp = cum + Bc;
         double* reg = comp + Bc;
         OCX_HIP(ocx_launch_gen_seek(base_seed, T, run0 + r0, nb, d, rs, ls, st));
-        OCX_HIP(hipMemsetAsync(th, 0, (size_t)nb * L1.Dp * 8, st));
+        OCX_HIP(hipMemsetAsync(th, 0, (size_t)nb * Lb.Dp * 8, st));
         OCX_HIP(hipMemsetAsync(cum, 0, (size_t)Bc * 2 * 8, st));
         for (int pass = 0; pass < 2; ++pass) {
             for (int64_t c = 0; c < nch; ++c) {

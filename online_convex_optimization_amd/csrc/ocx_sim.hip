@@ -324,6 +324,61 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// exact_ftl.py:280-303 `compute_prefix_actions` for the l2 ball, in the closed form of
+// the exact SOCP solution (regime as ocx_alg_kernel algo 2): actions[b][t] = FTL of
+// theta_t = −S_t = −Σ_{i<t} y_i z_i for t = 0..T, row-major [B][T+1][d].  The same step
+// arithmetic as algo 2, so replaying these actions reproduces ocx_ftl_exact's losses bit
+// for bit.  Writes are per-sequence rows (d contiguous doubles per lane group): this is
+// the drivers' small-batch API, not a bandwidth path.
+// ---------------------------------------------------------------------------
+template <int C, int P, bool CHAIN>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t d, int64_t G, double* __restrict__ actions, int* __restrict__ regime_out) {
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 64;
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;
+    const double* __restrict__ yp = yt + g * T * S + s;
+    double* __restrict__ arow = actions + (b < B ? b : 0) * (T + 1) * d + (int64_t)c * C;
+    const int jn = (int)std::max<int64_t>(0, std::min<int64_t>(C, d - (int64_t)c * C));
+
+    double th[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = 0.0;
+    bool linear = true;
+    for (int64_t t = 0; t <= T; ++t) {
+        double x[C];
+        ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+        if (b < B) {
+#pragma unroll
+            for (int j = 0; j < C; ++j)
+                if (j < jn) arow[t * d + j] = x[j];
+        }
+        if (t == T) break;
+        ocx_d2 z[K];
+        ocx_load_tile<C>(z, zp + t * tstride, kst);
+        const double yv = yp[t * S];
+        double p[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * ocx_zj(z, j);
+        const double zz = ocx_total<C, P, CHAIN>(p, lane);
+        linear = linear && zz <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+        const double gq = -yv;
+#pragma unroll
+        for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(z, j);
+    }
+    if (c == 0 && b < B && regime_out) regime_out[b] = linear ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------
 // Layout packing and small reductions
 // ---------------------------------------------------------------------------
 __global__ void ocx_pack_z_kernel(const double* __restrict__ z, double* __restrict__ zt,
@@ -410,6 +465,14 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
     return hipGetLastError();
 }
 
+template <int C, int P, bool CH>
+hipError_t launch_prefix_cp(const ocx_layout* L, const double* zt, const double* yt,
+                            double* actions, int* regime, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_prefix_actions_kernel<C, P, CH>), dim3(grid_for(L->G)),
+                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, actions, regime);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 bool ocx_supported_C(int C) {
@@ -444,6 +507,12 @@ hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double
     if (L->G == 0) return hipSuccess;
     OCX_DISPATCH(launch_replay_cp, L, zt, yt, at, cum, comp, st)
 }
+hipError_t ocx_launch_prefix_actions(const ocx_layout* L, const double* zt, const double* yt,
+                                     double* actions, int* regime, hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    OCX_DISPATCH(launch_prefix_cp, L, zt, yt, actions, regime, st)
+}
+
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
                            double* ytl, hipStream_t st) {
     const int64_t zn = L->z_elems, yn = L->y_elems;

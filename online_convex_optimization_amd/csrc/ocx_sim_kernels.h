@@ -20,6 +20,9 @@ hipError_t ocx_launch_smart_wave(const ocx_layout* L, const double* zt, const do
                                  hipStream_t st);
 hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double* yt,
                              const double* at, double* cum, double* comp, hipStream_t st);
+// exact FTL prefix actions [B][T+1][d] (closed form, l2 ball; ocx_sim.hip)
+hipError_t ocx_launch_prefix_actions(const ocx_layout* L, const double* zt, const double* yt,
+                                     double* actions, int* regime, hipStream_t st);
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
                            double* ytl, hipStream_t st);
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);

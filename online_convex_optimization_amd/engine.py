@@ -98,6 +98,14 @@ def replay_batch(z, y, actions, *, device: int = 0):
 NORMS = {"l2": 0}
 
 
+def _reject_out_of_regime(ok: np.ndarray) -> None:
+    if not ok.all():
+        bad = int(np.flatnonzero(~ok)[0])
+        raise NotImplementedError(
+            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
+            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+
+
 def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: int = 0,
                     check_regime: bool = True):
     """exact_ftl.py:280-333 (compute_prefix_actions + replay) for B sequences on the GPU,
@@ -120,12 +128,32 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: i
               ptr(act), rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq),
               int(device))
     ok = rg.astype(bool)
-    if check_regime and not ok.all():
-        bad = int(np.flatnonzero(~ok)[0])
-        raise NotImplementedError(
-            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
-            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+    if check_regime:
+        _reject_out_of_regime(ok)
     return cum, comp, act, ok
+
+
+def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: int = 0,
+                             check_regime: bool = True):
+    """exact_ftl.py:280-303 compute_prefix_actions for B sequences on the GPU
+    (include/ocx.h, ocx_ftl_prefix_actions_batch): actions [B, T+1, d] with actions[:, t]
+    the exact FTL solution of the first t rows, in the closed form of ftl_exact_batch.
+
+    Returns (actions, in_regime [B]); with ``check_regime`` a sequence outside the regime
+    raises NotImplementedError."""
+    if norm not in NORMS:
+        raise NotImplementedError(f"exact FTL for norm={norm!r}: only 'l2' is provided")
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    act = np.zeros((B, T + 1, d))
+    rg = np.zeros(B, dtype=np.int32)
+    _lib.call("ocx_ftl_prefix_actions_batch", ptr(z), ptr(y), B, T, d, NORMS[norm], ptr(act),
+              rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
+    ok = rg.astype(bool)
+    if check_regime:
+        _reject_out_of_regime(ok)
+    return act, ok
 
 
 def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, device: int = 0,
@@ -147,11 +175,8 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, de
               ptr(cmp_e), ptr(cmp_f) if with_ftl_comparator else None, ptr(act),
               rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
-    if check_regime and not ok.all():
-        bad = int(np.flatnonzero(~ok)[0])
-        raise NotImplementedError(
-            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
-            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+    if check_regime:
+        _reject_out_of_regime(ok)
     out = {"ftrl": cr - cmp_e, "exact": ce - cmp_e, "cum_ftrl": cr, "cum_exact": ce,
            "comp": cmp_e, "action": act, "in_regime": ok}
     if with_ftl_comparator:
@@ -234,6 +259,7 @@ class DeviceBatch:
         self.device = torch.device("cuda", device)
         with torch.cuda.device(self.device):
             self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.device(self.device), torch.cuda.stream(self.stream):
             self.z = torch.empty(max(self.L.z_elems, 1), dtype=torch.float64, device=self.device)
             self.y = torch.empty(max(self.L.y_elems, 1), dtype=torch.float64, device=self.device)
             self.regret = torch.zeros(max(B, 1), dtype=torch.float64, device=self.device)
@@ -244,6 +270,21 @@ class DeviceBatch:
     @property
     def _sp(self):
         return ctypes.c_void_p(self.stream.cuda_stream)
+
+    def _on_stream(self):
+        """Context that makes self.stream current on this device: helper tensors (seeds,
+        thresholds, device-side dtype conversions) are then produced in the same stream
+        order as the HIP kernels that read them."""
+        return self.torch.cuda.stream(self.stream)
+
+    def _hold(self, *tensors):
+        """Keep helper tensors alive for the kernels queued on self.stream, and tell the
+        caching allocator they are in use there (record_stream), so their memory is not
+        handed out again before those kernels ran even if the next call replaces them."""
+        for t in tensors:
+            if t is not None and t.is_cuda:
+                t.record_stream(self.stream)
+        return tensors
 
     def _lp(self):
         return ctypes.byref(self.L)
@@ -264,31 +305,35 @@ class DeviceBatch:
         fam = self.FAMILIES[family] if isinstance(family, str) else int(family)
         rs = si = None
         if fam in (1, 2):
-            rs = torch.as_tensor(np.asarray(run_seeds, dtype=np.uint64).astype(np.int64)
-                                 ).to(self.device)
-            si = torch.as_tensor(np.asarray(stream_ids, dtype=np.uint64).astype(np.int64)
-                                 ).to(self.device)
+            with self._on_stream():
+                rs = torch.as_tensor(np.asarray(run_seeds, dtype=np.uint64).astype(np.int64)
+                                     ).to(self.device)
+                si = torch.as_tensor(np.asarray(stream_ids, dtype=np.uint64).astype(np.int64)
+                                     ).to(self.device)
             if rs.numel() != self.L.B or si.numel() != self.L.B:
                 raise ValueError("need one run seed and one stream id per sequence")
         _lib.call("ocx_dev_gen_family", self._lp(), fam,
                   rs.data_ptr() if rs is not None else None,
                   si.data_ptr() if si is not None else None, float(p), int(block_len),
                   self.z.data_ptr(), self.y.data_ptr(), self._sp)
-        self._keep_seeds = (rs, si)
+        self._keep_seeds = self._hold(rs, si)
         return self
 
     def pack(self, z, y):
         """Copy host/device arrays z [B,T,d], y [B,T] into the tiled layout."""
         torch = self.torch
-        zt = torch.as_tensor(np.ascontiguousarray(z, dtype=np.float64) if isinstance(z, np.ndarray)
-                             else z).to(self.device, torch.float64).contiguous()
-        yt = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float64) if isinstance(y, np.ndarray)
-                             else y).to(self.device, torch.float64).contiguous()
+        with self._on_stream():
+            zt = torch.as_tensor(np.ascontiguousarray(z, dtype=np.float64)
+                                 if isinstance(z, np.ndarray) else z
+                                 ).to(self.device, torch.float64).contiguous()
+            yt = torch.as_tensor(np.ascontiguousarray(y, dtype=np.float64)
+                                 if isinstance(y, np.ndarray) else y
+                                 ).to(self.device, torch.float64).contiguous()
         if tuple(zt.shape) != (self.L.B, self.L.T, self.L.d) or tuple(yt.shape) != (self.L.B, self.L.T):
             raise ValueError("z/y shape does not match the batch")
         _lib.call("ocx_dev_pack", self._lp(), zt.data_ptr(), yt.data_ptr(), self.z.data_ptr(),
                   self.y.data_ptr(), self._sp)
-        self._keep = (zt, yt)
+        self._keep = self._hold(zt, yt)
         return self
 
     def simulate_alg(self, alg_flag: int = 0, eta0: float = SQRT2, comparator=None,
@@ -302,12 +347,13 @@ class DeviceBatch:
         return self.regret
 
     def simulate_smart(self, thresh, eta0: float = SQRT2, switch_step=None):
-        th = self.torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
-                                                  (self.L.B,)).copy()).to(self.device)
+        with self._on_stream():
+            th = self.torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
+                                                      (self.L.B,)).copy()).to(self.device)
         sp = switch_step.data_ptr() if switch_step is not None else None
         _lib.call("ocx_dev_simulate_smart", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, self._sp)
-        self._keep_th = th
+        self._keep_th = self._hold(th)
         return self.regret
 
     def ftl_exact(self, cmp_action=None, regime=None):
@@ -317,7 +363,8 @@ class DeviceBatch:
         regime flags (allocated when None).  Returns regime."""
         torch = self.torch
         if regime is None:
-            regime = torch.zeros(max(self.L.B, 1), dtype=torch.int32, device=self.device)
+            with self._on_stream():
+                regime = torch.zeros(max(self.L.B, 1), dtype=torch.int32, device=self.device)
         _lib.call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(), 0,
                   self.cum.data_ptr(), self.comp.data_ptr(),
                   cmp_action.data_ptr() if cmp_action is not None else None,
@@ -331,10 +378,11 @@ class DeviceBatch:
         regime flags."""
         torch = self.torch
         n = max(self.L.B, 1)
-        if self.cum_exact is None:
-            self.cum_exact = torch.zeros(n, dtype=torch.float64, device=self.device)
-        if regime is None:
-            regime = torch.zeros(n, dtype=torch.int32, device=self.device)
+        with self._on_stream():
+            if self.cum_exact is None:
+                self.cum_exact = torch.zeros(n, dtype=torch.float64, device=self.device)
+            if regime is None:
+                regime = torch.zeros(n, dtype=torch.int32, device=self.device)
         _lib.call("ocx_dev_ftrl_vs_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
@@ -344,7 +392,9 @@ class DeviceBatch:
 
     def max_regret(self, out=None):
         torch = self.torch
-        out = out if out is not None else torch.zeros(1, dtype=torch.float64, device=self.device)
+        if out is None:
+            with self._on_stream():
+                out = torch.zeros(1, dtype=torch.float64, device=self.device)
         _lib.call("ocx_dev_max_regret", self.regret.data_ptr(), int(self.L.B), out.data_ptr(),
                   self._sp)
         return out

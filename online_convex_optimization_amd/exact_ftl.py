@@ -1,18 +1,24 @@
-"""Drop-in for the FTRL / replay half of the reference's ``exact_ftl.py``.
+"""Drop-in for the reference's ``exact_ftl.py`` (the module ``exact_ftl_driver.py:24-29``
+imports): ``ExactFTLNoClip``, ``compute_prefix_actions``, ``replay_exact_ftl``,
+``run_ftrl``, ``run_ftl_exact``, ``simulate`` and ``RunResult``, with the reference's
+names, signatures and errors.  The FTRL loop (exact_ftl.py:230-277), the replay
+(:306-333) and the exact FTL solutions all run in the HIP kernels.
 
-Same names and signatures for ``RunResult``, ``run_ftrl``, ``replay_exact_ftl``,
-``simulate`` and ``run_ftl_exact``; the FTRL loop (exact_ftl.py:230-277) and the
-replay (:306-333) run in the HIP kernels.
+Exact FTL (the cvxpy SOCP of ``ExactFTLNoClip``, exact_ftl.py:62-193) is solved on the
+GPU in closed form for the l2 ball whenever the data satisfy ||z_t|| <= 1 and
+y_t = ±1 — every sequence family and adversary of the reference does: there
+½Σ|z_i·x − y_i| = ½(t − x·S_t) on the ball, so the minimiser is S_t/||S_t||,
+S_t = Σ_{i<t} y_i z_i (engine.ftl_prefix_actions_batch / ftl_exact_batch).
 
-The exact FTL solutions (the cvxpy SOCP of ``ExactFTLNoClip``, exact_ftl.py:62-193)
-are computed on the GPU in closed form for the l2 ball whenever the data satisfy
-||z_t|| <= 1 and y_t = ±1 — every sequence family and adversary of the reference does:
-there ½Σ|z_i·x − y_i| is linear on the ball and its minimiser is S_t/||S_t||,
-S_t = Σ_{i<t} y_i z_i (engine.ftl_exact_batch).  Outside that regime, and for the l1 /
-linf balls, the general SOCP is out of scope: cvxpy is absent, so its results are
-unpinned and those calls raise ``NotImplementedError`` unless the caller
-supplies ``comparator_action`` / ``prefix_actions`` or a solver object with the
-reference's methods.
+* Degenerate prefixes (S_t = 0, e.g. the empty prefix): every point of the ball is
+  optimal; the engine returns 0 (cvxpy's interior-point choice is solver-dependent).
+* Outside that regime, and for the l1 / linf balls, the general SOCP/LP is out of scope
+  (DESIGN.md §7): those calls raise ``NotImplementedError``.  A caller can still pass
+  ``comparator_action`` / ``prefix_actions`` or any solver object with the reference's
+  methods (``reset_buffers`` / ``append_row`` / ``solve_prefix_from_full``).
+* Parity of the closed form against cvxpy is **unpinned**: cvxpy is absent here and the
+  reference ships no fixture for it.  It is checked against the C oracle's closed form
+  and independently against scipy SLSQP on the CPU (tests/test_exact_comparator_cpu.py).
 """
 from __future__ import annotations
 
@@ -44,27 +50,140 @@ def _ensure_float64_contiguous(arr) -> np.ndarray:
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
-class ExactFTLNoClip:
-    """exact_ftl.py:62-193 — the cvxpy SOCP/LP exact-FTL solver.  Not provided: cvxpy is
-    absent and no reference oracle pins its outputs."""
+_NORMS = ("l2", "linf", "l1")
 
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError(
-            "ExactFTLNoClip (cvxpy SOCP comparator) is out of scope; pass comparator_action "
-            "or prefix_actions instead")
+
+class ExactFTLNoClip:
+    """exact_ftl.py:62-193: exact FTL over the unit norm ball, one reusable solver per
+    (d, T_max) holding the current prefix in ``_Z_buf`` / ``_y_buf`` / ``_w_buf`` as the
+    reference does.  Every solve runs on the GPU in closed form (module docstring); the
+    ``solver`` / ``solver_opts`` arguments are accepted and kept for signature parity
+    (no cvxpy backend is involved).
+
+    ``norm='l2'`` only: 'linf' / 'l1' raise NotImplementedError, anything else
+    ValueError (exact_ftl.py:101-102)."""
+
+    def __init__(self, d: int, T_max: int, *, norm: Literal["l2", "linf", "l1"] = "l2",
+                 solver: Optional[str] = None, solver_opts: Optional[dict] = None) -> None:
+        self.d = int(d)
+        self.T_max = int(T_max)
+        self.norm = norm
+        self.solver = solver
+        self.solver_opts = {} if solver_opts is None else dict(solver_opts)
+        if norm not in _NORMS:
+            raise ValueError("norm must be one of {'l2','linf','l1'}")
+        if norm != "l2":
+            raise NotImplementedError(
+                f"exact FTL over the {norm} ball (an LP in the reference) is out of scope; "
+                "only the l2 ball is solved (closed form on the GPU)")
+        self._Z_buf = np.zeros((self.T_max, self.d), dtype=np.float64)
+        self._y_buf = np.zeros(self.T_max, dtype=np.float64)
+        self._w_buf = np.zeros(self.T_max, dtype=np.float64)
+        self._last_length = 0
+
+    # -- solves ---------------------------------------------------------------
+    def _solve_length(self, z_src: np.ndarray, y_src: np.ndarray, length: int) -> np.ndarray:
+        """Exact FTL solution of the first ``length`` rows (GPU, closed form)."""
+        _, _, act, _ = _engine.ftl_exact_batch(z_src[None, :length], y_src[None, :length],
+                                               norm=self.norm, device=_fa._DEVICE)
+        return act[0]
+
+    def _solve_current(self) -> np.ndarray:
+        """exact_ftl.py:120-128 for the cached prefix."""
+        return self._solve_length(self._Z_buf, self._y_buf, self._last_length)
+
+    def reset_buffers(self) -> None:
+        """exact_ftl.py:130-139."""
+        self._Z_buf.fill(0.0)
+        self._y_buf.fill(0.0)
+        self._w_buf.fill(0.0)
+        self._last_length = 0
+
+    def append_row(self, z_row: np.ndarray, y_val: float) -> np.ndarray:
+        """exact_ftl.py:141-150: append one example to the cached prefix and solve."""
+        if self._last_length >= self.T_max:
+            raise ValueError("sequence longer than T_max")
+        idx = self._last_length
+        self._Z_buf[idx] = z_row
+        self._y_buf[idx] = y_val
+        self._w_buf[idx] = 1.0
+        self._last_length += 1
+        return self._solve_current()
+
+    def _set_prefix(self, z_source: np.ndarray, y_source: np.ndarray, length: int) -> None:
+        """exact_ftl.py:152-169."""
+        t = int(length)
+        if t < 0 or t > self.T_max:
+            raise ValueError("length must be between 0 and T_max inclusive")
+        if t > 0:
+            np.copyto(self._Z_buf[:t], z_source[:t])
+            np.copyto(self._y_buf[:t], y_source[:t])
+            self._w_buf[:t] = 1.0
+        if t < self._last_length:
+            tail = slice(t, self._last_length)
+            self._Z_buf[tail] = 0.0
+            self._y_buf[tail] = 0.0
+            self._w_buf[tail] = 0.0
+        self._last_length = t
+
+    def solve_prefix_from_full(self, z_full: np.ndarray, y_full: np.ndarray,
+                               length: int) -> np.ndarray:
+        """exact_ftl.py:171-181: solve over the first ``length`` rows of z_full/y_full."""
+        z_src = _ensure_float64_contiguous(z_full)
+        y_src = _ensure_float64_contiguous(y_full)
+        self._set_prefix(z_src, y_src, length)
+        return self._solve_current()
+
+    def solve_prefix(self, z_prefix: np.ndarray, y_prefix: np.ndarray) -> np.ndarray:
+        """exact_ftl.py:183-193."""
+        z_src = _ensure_float64_contiguous(z_prefix)
+        y_src = _ensure_float64_contiguous(y_prefix)
+        t, d = z_src.shape
+        if d != self.d:
+            raise ValueError(f"Expected {self.d}-dimensional data, got {d}")
+        if t > self.T_max:
+            raise ValueError("prefix longer than T_max")
+        self._set_prefix(z_src, y_src, t)
+        return self._solve_current()
+
+
+def compute_prefix_actions(solver, z: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """exact_ftl.py:280-303: exact FTL solutions for every prefix length 0..T → [T+1, d].
+
+    With this module's ``ExactFTLNoClip`` all T+1 solutions come from one GPU launch
+    (ocx_ftl_prefix_actions_batch) and the solver is left holding the whole sequence, as
+    after the reference's append loop.  Any other solver object is driven row by row
+    through its ``reset_buffers`` / ``append_row``, as the reference does."""
+    z_arr = _ensure_float64_contiguous(z)
+    y_arr = _ensure_float64_contiguous(y)
+    T, d = z_arr.shape
+    if solver.d != d:
+        raise ValueError(f"Solver dimension {solver.d} incompatible with data dimension {d}")
+    if solver.T_max < T:
+        raise ValueError("Solver T_max is smaller than sequence length")
+    if isinstance(solver, ExactFTLNoClip):
+        actions, _ = _engine.ftl_prefix_actions_batch(z_arr[None], y_arr[None], norm=solver.norm,
+                                                      device=_fa._DEVICE)
+        solver._set_prefix(z_arr, y_arr, T)
+        return actions[0]
+    actions = np.zeros((T + 1, d), dtype=np.float64)
+    solver.reset_buffers()
+    for idx in range(T):
+        actions[idx + 1] = solver.append_row(z_arr[idx], float(y_arr[idx]))
+    return actions
 
 
 def _simulate_ftrl(z_arr, y_arr, *, eta0, comparator_action=None, comparator_solver=None,
                    norm="l2", solver_name=None, solver_opts=None) -> RunResult:
-    """exact_ftl.py:230-277 on the GPU."""
+    """exact_ftl.py:230-277 on the GPU: the FTRL loop, then the comparator loss of the
+    caller's action or of the solver's solution over the whole sequence."""
     T, d = z_arr.shape
     if comparator_action is None:
-        if comparator_solver is not None:
-            comparator_action = comparator_solver.solve_prefix_from_full(z_arr, y_arr, T)
-        else:  # exact SOCP solution of the whole sequence, closed form on the GPU
-            _, _, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
-                                                   device=_fa._DEVICE)
-            comparator_action = act[0]
+        solver = comparator_solver
+        if solver is None:
+            solver = ExactFTLNoClip(d=d, T_max=T, norm=norm, solver=solver_name,
+                                    solver_opts=solver_opts)
+        comparator_action = solver.solve_prefix_from_full(z_arr, y_arr, T)
     comp_vec = _ensure_float64_contiguous(comparator_action)
     if comp_vec.shape != (d,):
         raise ValueError(f"comparator_action must have shape ({d},)")
@@ -96,18 +215,12 @@ def replay_exact_ftl(z: np.ndarray, y: np.ndarray, actions: np.ndarray) -> RunRe
                      comp_loss=float(comp[0]), x_last=acts[T].copy())
 
 
-def _prefix_actions_from_solver(ftl_solver, z_arr, y_arr) -> np.ndarray:
-    """exact_ftl.py:280-303 compute_prefix_actions, driving a caller-supplied solver."""
-    T, d = z_arr.shape
-    actions = np.zeros((T + 1, d), dtype=np.float64)
-    ftl_solver.reset_buffers()
-    for i in range(T):
-        actions[i + 1] = ftl_solver.append_row(z_arr[i], float(y_arr[i]))
-    return actions
-
-
 def _ftl_exact_gpu(z_arr, y_arr, norm) -> RunResult:
-    """exact_ftl.py:423-453 with the prefix actions solved on the GPU (closed form)."""
+    """exact_ftl.py:423-453 without materialising the T+1 actions: prefix solutions and
+    replay in one kernel (closed form; bit-identical to replaying
+    compute_prefix_actions' output)."""
+    if norm not in _NORMS:
+        raise ValueError("norm must be one of {'l2','linf','l1'}")
     cum, comp, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
                                                 device=_fa._DEVICE)
     return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - comp[0]),
@@ -126,7 +239,7 @@ def simulate(z, y, *, algo: Literal["ftrl", "ftl_exact"] = "ftl_exact", eta0: fl
         if prefix_actions is None and ftl_solver is None:
             return _ftl_exact_gpu(z_arr, y_arr, norm)
         if prefix_actions is None:
-            prefix_actions = _prefix_actions_from_solver(ftl_solver, z_arr, y_arr)
+            prefix_actions = compute_prefix_actions(ftl_solver, z_arr, y_arr)
         return replay_exact_ftl(z_arr, y_arr, prefix_actions)
     if algo == "ftrl":
         return _simulate_ftrl(z_arr, y_arr, eta0=eta0, comparator_action=comparator_action,
@@ -147,19 +260,17 @@ def run_ftrl(z, y, *, eta0: float = 1.0, norm: Literal["l2", "linf", "l1"] = "l2
 def run_ftl_exact(z, y, *, norm="l2", solver=None, solver_opts=None, ftl_solver=None,
                   prefix_actions: Optional[np.ndarray] = None, return_actions: bool = False
                   ) -> RunResult | Tuple[RunResult, np.ndarray]:
-    """exact_ftl.py:423-453.  Without ``prefix_actions`` or ``ftl_solver`` the prefix
-    actions are solved on the GPU (closed form, l2 ball) and replayed in the same kernel;
-    the T+1 actions are not materialised, so ``return_actions=True`` needs one of the two."""
+    """exact_ftl.py:423-453."""
     z_arr = _ensure_float64_contiguous(z)
     y_arr = _ensure_float64_contiguous(y)
-    actions = prefix_actions
-    if actions is None and ftl_solver is None and not return_actions:
+    if prefix_actions is None and ftl_solver is None and not return_actions:
         return _ftl_exact_gpu(z_arr, y_arr, norm)
+    actions = prefix_actions
     if actions is None:
-        if ftl_solver is None:
-            raise NotImplementedError("return_actions=True needs prefix_actions or a solver "
-                                      "object (the GPU path does not materialise T+1 actions)")
-        actions = _prefix_actions_from_solver(ftl_solver, z_arr, y_arr)
+        T, d = z_arr.shape
+        solver_obj = ftl_solver if ftl_solver is not None else ExactFTLNoClip(
+            d=d, T_max=T, norm=norm, solver=solver, solver_opts=solver_opts)
+        actions = compute_prefix_actions(solver_obj, z_arr, y_arr)
     result = replay_exact_ftl(z_arr, y_arr, actions)
     if return_actions:
         return result, actions

@@ -52,11 +52,15 @@ def gT_sweep_distributed(T_grid: Sequence[int], runs: int, *, base_seed: int = 0
     """empirical_worst_case_thresholds across the ranks of the default process group.
 
     ``compute(T, run0, count)`` returns this rank's regrets (default: regenerate and
-    simulate on the local GPU through engine.gT_regrets).  Returns, on every rank,
-    {T: (g(T), regrets[runs] in run order)}."""
+    simulate on the local GPU through engine.gT_regrets).  ``device`` is where the gather
+    runs: the rank's current GPU under the "nccl" (RCCL) backend, host memory otherwise.
+    Returns, on every rank, {T: (g(T), regrets[runs] in run order)}."""
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
+    if device is None and dist.get_backend() == "nccl":
+        # RCCL gathers device tensors only: collect on this rank's GPU
+        device = torch.device("cuda", torch.cuda.current_device())
     if compute is None:
         from . import engine
         dev_index = torch.cuda.current_device()

@@ -192,6 +192,27 @@ int oc_ftl_exact(const double *z, const double *y, int64_t T, int64_t d, double 
     return 0;
 }
 
+/* exact_ftl.py:280-303 `compute_prefix_actions` for the l2 ball in the closed form of
+ * oc_ftl_exact: actions [T+1][d], actions[t] = FTL(theta_t), theta_t = -S_t. */
+int oc_ftl_prefix_actions(const double *z, const double *y, int64_t T, int64_t d,
+                          double *actions, int *regime) {
+    double *theta = (double *)calloc((size_t)(d > 0 ? d : 1), sizeof(double));
+    if (!theta) return -1;
+    int linear = 1;
+    for (int64_t t = 0; t <= T; ++t) {
+        oc_action_ftl(theta, d, actions + t * d);
+        if (t == T) break;
+        const double *zt = z + t * d;
+        double zz = 0.0;
+        for (int64_t j = 0; j < d; ++j) zz += zt[j] * zt[j];
+        if (!(zz <= 1.0 + 1e-6 && fabs(y[t]) == 1.0)) linear = 0;
+        for (int64_t j = 0; j < d; ++j) theta[j] += (-y[t]) * zt[j];
+    }
+    if (regime) *regime = linear;
+    free(theta);
+    return 0;
+}
+
 /* exact_ftl.py:306-333 `replay_exact_ftl` loop: actions is [T+1][d]. */
 int oc_replay(const double *z, const double *y, int64_t T, int64_t d, const double *actions,
               double *cum_loss_out) {

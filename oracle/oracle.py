@@ -67,6 +67,8 @@ def lib():
         L.oc_max_threads.restype = ctypes.c_int
         L.oc_ftl_exact.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp, _dp,
                                    ctypes.POINTER(ctypes.c_int)]
+        L.oc_ftl_prefix_actions.argtypes = [_dp, _dp, ctypes.c_int64, ctypes.c_int64, _dp,
+                                            ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -149,6 +151,18 @@ def ftl_exact_closed_form(z, y):
     lib().oc_ftl_exact(_ptr(z), _ptr(y), T, d, _ptr(out[0:1]), _ptr(out[1:2]), _ptr(a),
                        ctypes.byref(rg))
     return float(out[0]), float(out[1]), a, bool(rg.value)
+
+
+def ftl_prefix_actions(z, y):
+    """exact_ftl.py:280-303 (l2 ball) in closed form → (actions [T+1, d], in_regime).
+    See oc_ftl_prefix_actions in ocx_oracle.c."""
+    z = _f64(z)
+    y = _f64(y)
+    T, d = z.shape
+    a = np.zeros((T + 1, d))
+    rg = ctypes.c_int(0)
+    lib().oc_ftl_prefix_actions(_ptr(z), _ptr(y), T, d, _ptr(a), ctypes.byref(rg))
+    return a, bool(rg.value)
 
 
 def comparator_loss_blas(z, y, x) -> float:

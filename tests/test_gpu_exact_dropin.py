@@ -1,0 +1,115 @@
+"""GPU: the exact_ftl drop-in's solver objects (ExactFTLNoClip, compute_prefix_actions,
+run_ftrl(comparator_solver=...), replay_exact_ftl) against the C oracle's closed form,
+bit for bit, on the reference's random i.i.d. family (sequence_generation.py:55-70) and
+the g(T) adversary — the data exact_ftl_driver.py:80-186 feeds them.
+
+The closed form is the exact SOCP solution in the regime every reference family lives in
+(||z_t|| <= 1, y = ±1); against cvxpy itself it is parity-unpinned (cvxpy is absent)."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+SQ2 = math.sqrt(2)
+
+
+@pytest.fixture(scope="module")
+def ef():
+    from online_convex_optimization_amd import _lib, exact_ftl
+    assert _lib.device_count() >= 1
+    return exact_ftl
+
+
+@pytest.mark.parametrize("T,rep", [(1, 0), (100, 0), (257, 2), (600, 1)])
+def test_compute_prefix_actions_matches_oracle(ef, T, rep):
+    z, y, _ = O.random_iid_sample(2025, T, rep)
+    solver = ef.ExactFTLNoClip(d=z.shape[1], T_max=T)
+    acts = ef.compute_prefix_actions(solver, z, y)
+    want, ok = O.ftl_prefix_actions(z, y)
+    assert ok and acts.shape == (T + 1, z.shape[1])
+    assert np.array_equal(acts, want)
+    assert not acts[0].any()  # empty prefix -> 0
+    assert solver._last_length == T  # left holding the sequence, as after the append loop
+    # replay of these actions == the fused exact-FTL kernel == the oracle replay
+    rp = ef.replay_exact_ftl(z, y, acts)
+    fused = ef.run_ftl_exact(z, y)
+    assert rp.cum_loss == fused.cum_loss == O.replay_cum_loss(z, y, want)
+    assert rp.comp_loss == fused.comp_loss and np.array_equal(rp.x_last, fused.x_last)
+    assert rp.comp_loss == O.ftl_exact_closed_form(z, y)[1]
+
+
+def test_append_row_and_prefix_solves_match(ef):
+    z, y, _ = O.random_iid_sample(4050, 40, 0)
+    want, _ = O.ftl_prefix_actions(z, y)
+    s = ef.ExactFTLNoClip(5, 40)
+    s.reset_buffers()
+    for t in range(40):
+        assert np.array_equal(s.append_row(z[t], float(y[t])), want[t + 1]), t
+    with pytest.raises(ValueError):
+        s.append_row(z[0], 1.0)
+    assert np.array_equal(s.solve_prefix_from_full(z, y, 17), want[17])
+    assert np.array_equal(s.solve_prefix(z[:23], y[:23]), want[23])
+    assert np.array_equal(s.solve_prefix_from_full(z, y, 0), want[0])
+
+
+def test_run_ftrl_with_comparator_solver(ef):
+    """exact_ftl_driver.py:72-111: g(T) with run_ftrl(comparator_solver=ExactFTLNoClip)."""
+    T = 300
+    solver = ef.ExactFTLNoClip(d=5, T_max=T)
+    for run in range(4):
+        z, y = O.gT_sample(0, T, run, 5)
+        rr = ef.run_ftrl(z, y, eta0=SQ2, comparator_solver=solver)
+        _, _, a, ok = O.ftl_exact_closed_form(z, y)
+        assert ok
+        ref = O.simulate_alg_full(z, y, 0, SQ2, comparator=a)
+        assert (rr.regret, rr.cum_loss, rr.comp_loss) == tuple(ref[:3]), run
+        # the default (no solver, no action) builds its own solver: same result
+        assert ef.run_ftrl(z, y, eta0=SQ2).regret == rr.regret
+
+
+def test_exact_driver_loop_body(ef):
+    """exact_ftl_driver.py:157-186 loop body verbatim in structure: prefix actions from a
+    cached solver, FTRL against actions[-1], replay of the actions."""
+    from online_convex_optimization_amd.sequence_generation import CASES
+    sampler = CASES["Random i.i.d. (separable)"](run_seed=2025)
+    cache = {}
+    for T in (100, 200):
+        for rep in range(3):
+            z, y, _ = sampler(T, rep=rep)
+            z_arr = np.ascontiguousarray(z, dtype=np.float64)
+            y_arr = np.ascontiguousarray(y, dtype=np.float64)
+            key = (z_arr.shape[1], T)
+            solver = cache.setdefault(key, ef.ExactFTLNoClip(d=key[0], T_max=T))
+            actions = ef.compute_prefix_actions(solver, z_arr, y_arr)
+            ftrl = ef.run_ftrl(z_arr, y_arr, eta0=SQ2, comparator_action=actions[-1])
+            ftl = ef.replay_exact_ftl(z_arr, y_arr, actions)
+            c, p, a, ok = O.ftl_exact_closed_form(z_arr, y_arr)
+            assert ok and np.array_equal(actions[-1], a)
+            assert ftl.regret == c - p
+            assert ftrl.regret == O.simulate_alg_full(z_arr, y_arr, 0, SQ2, comparator=a)[0]
+
+
+def test_out_of_regime_rejected(ef):
+    z, y, _ = O.random_iid_sample(2025, 50, 0)
+    with pytest.raises(NotImplementedError):
+        ef.compute_prefix_actions(ef.ExactFTLNoClip(5, 50), 3.0 * z, y)
+    with pytest.raises(NotImplementedError):
+        ef.ExactFTLNoClip(5, 50).solve_prefix_from_full(z, 0.5 * y, 50)
+
+
+def test_prefix_actions_batch_lane_splits(ef):
+    from online_convex_optimization_amd import engine
+    rng = np.random.default_rng(5)
+    for B, T, d in ((13, 90, 64), (3, 33, 1024), (70, 20, 3)):
+        z = rng.standard_normal((B, T, d))
+        z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+        y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+        want = np.stack([O.ftl_prefix_actions(z[b], y[b])[0] for b in range(B)])
+        for P in (1, -1, -4):
+            if P != 1 and d > 64 * abs(P):
+                continue
+            acts, ok = engine.ftl_prefix_actions_batch(z, y, lanes_per_seq=P)
+            assert ok.all() and np.array_equal(acts, want), (B, T, d, P)

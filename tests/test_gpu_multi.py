@@ -1,0 +1,99 @@
+"""GPU: the product's multi-device code paths on a one-GPU box.
+
+* parallel.gT_sweep_distributed with its DEFAULT compute (engine.gT_regrets on the rank's
+  GPU), world_size 2 over gloo, both ranks on device 0, ragged shards;
+* the same over the "nccl" backend (RCCL) with world_size 1: RCCL initialisation and the
+  device all-gather run for real (two ranks cannot share one GPU under RCCL);
+* engine.gT_sweep(devices=[0, 0]): one process driving a device list from threads.
+
+Each is compared with one engine.gT_regrets call over all runs and with the oracle on
+sampled runs.  The sequences are independent streams _rng(seed, T, run)
+(fast_algorithms.py:254-257), so sharding must be bit-invisible."""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+SQ2 = math.sqrt(2)
+T_GRID, RUNS, D = [40, 257], 37, 16
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, backend, q):
+    import torch
+    import torch.distributed as dist
+    from online_convex_optimization_amd.parallel import gT_sweep_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = gT_sweep_distributed(T_GRID, RUNS, base_seed=3, d=D)
+        q.put((rank, {T: (g, regs.tolist()) for T, (g, regs) in res.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, backend):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        results = dict(q.get(timeout=90) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    return results
+
+
+@pytest.fixture(scope="module")
+def reference():
+    from online_convex_optimization_amd import engine
+    ref = {T: engine.gT_regrets(T, RUNS, base_seed=3, d=D) for T in T_GRID}
+    for T in T_GRID:
+        for r in (0, RUNS // 2, RUNS - 1):
+            z, y = O.gT_sample(3, T, r, D)
+            assert ref[T][r] == O.simulate_alg(z, y, 0, SQ2)
+    return ref
+
+
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (1, "nccl")])
+def test_gT_sweep_distributed_default_compute(reference, world, backend):
+    results = _run(world, backend)
+    for rank in range(world):
+        for T in T_GRID:
+            g, regs = results[rank][T]
+            assert np.array_equal(np.array(regs), reference[T]), (backend, rank, T)
+            assert g == max(0.0, float(reference[T].max()))
+
+
+def test_gT_sweep_device_list(reference):
+    from online_convex_optimization_amd import engine
+    out = engine.gT_sweep(T_GRID, RUNS, base_seed=3, d=D, devices=[0, 0])
+    for T in T_GRID:
+        g, regs = out[T]
+        assert np.array_equal(regs, reference[T])
+        assert g == max(0.0, float(reference[T].max()))

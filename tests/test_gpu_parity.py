@@ -332,6 +332,25 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
             assert chunked[r] == ref
 
 
+@pytest.mark.parametrize("P", [1, 0])
+def test_streamed_gT_ragged_last_batch(ocx, monkeypatch, P):
+    """More runs than one streamed batch (131 072) with a short last batch: the last batch
+    gets its own lane layout (d=5: 1 lane x 6 coordinates for the full batches, 4 x 2 for
+    100 sequences), so theta must be zeroed with that batch's row width."""
+    eng = ocx["engine"]
+    T, d, runs = 40, 5, 131072 + 100
+    whole = eng.gT_regrets(T, runs, base_seed=6, d=d, lanes_per_seq=P)
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(0.1))     # streamed, a few T-chunks
+    monkeypatch.setenv("OCX_MIN_RESIDENT", str(1 << 30))
+    chunked = eng.gT_regrets(T, runs, base_seed=6, d=d, lanes_per_seq=P)
+    # butterfly sums follow each batch's lane split, so only exact mode is layout-invariant
+    assert np.array_equal(whole, chunked) if P == 1 else close(chunked, whole)
+    for r in (0, 131071, 131072, runs - 1):
+        z, y = O.gT_sample(6, T, r, d)
+        ref = O.simulate_alg(z, y, 0, SQ2)
+        assert close(chunked[r], ref) if P == 0 else chunked[r] == ref
+
+
 @pytest.mark.parametrize("T,d,runs", [(50, 64, 700), (2, 1024, 3000)])
 def test_resident_batching_is_invisible(ocx, monkeypatch, T, d, runs):
     """Resident g(T) batches of any size (exact mode: lanes chosen per batch size; d=1024,
