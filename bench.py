@@ -43,8 +43,10 @@ def parse():
     ap.add_argument("--B", type=int, default=32768, help="sequences per GPU (resident batch)")
     ap.add_argument("--T", type=int, default=10000)
     ap.add_argument("--d", type=int, default=64)
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="lanes_per_seq (include/ocx.h): 1 = exact mode (bit-identical to the "
+    ap.add_argument("--lanes", type=int, default=128,
+                    help="lanes_per_seq (include/ocx.h): 128 = OCX_LANES_BEST (default: exact "
+                         "layout where it streams at the roofline, butterfly sums where exact "
+                         "chains are latency-bound), 1 = exact mode (bit-identical to the "
                          "reference, auto lanes), 0 = auto with butterfly sums, k / -k explicit")
     ap.add_argument("--e2e-steps", type=int, default=3,
                     help="untimed-for-the-metric batches of generation + simulation reported "
@@ -262,7 +264,8 @@ def main():
                                    "resident batches of B per GPU)",
                        "B_per_gpu": B, "T": T, "d": d, "lanes_per_seq": int(db.L.P),
                        "coords_per_lane": int(db.L.C),
-                       "sums": "exact (sequential order)" if (a.lanes == 1 or a.lanes < 0)
+                       "lanes_mode": {128: "best", 1: "exact", 0: "auto"}.get(a.lanes, str(a.lanes)),
+                       "sums": "exact (sequential order)" if (db.L.P == 1 or db.L.chain)
                                else "butterfly",
                        "parallelism": f"dp{world}",
                        "z_bytes_per_gpu": db.z_bytes},

@@ -27,8 +27,15 @@
  *              <= 4 lanes unless d needs more): every sum in the reference's
  *              sequential order, so results are bit-identical;
  *       -k     exact with k lanes; for k > 1 the running sum is handed from lane to
- *              lane (layout.chain = 1).
+ *              lane (layout.chain = 1);
+ *       OCX_LANES_BEST (128)  per workload: the exact layout (value 1) wherever its
+ *              lane chains are short (fewer than 8 lanes per sequence), where the
+ *              kernels stream at the HBM roofline; butterfly sums otherwise (d >= 512,
+ *              or few-wave batches such as the capacity-limited T = 1e5 g(T) batch),
+ *              where a chain of 8+ lanes leaves the kernel latency-bound.  Results are
+ *              bit-identical where the exact layout is kept, ~1e-16 relative elsewhere.
  */
+#define OCX_LANES_BEST 128
 #ifndef OCX_H_
 #define OCX_H_
 
@@ -76,7 +83,7 @@ int ocx_device_count(int* count);
  * (grown on demand, kept between calls).  Safe between calls; the next call regrows it.
  * Use before allocating large device buffers of one's own (engine.DeviceBatch). */
 int ocx_release_buffers(int device);
-/* Fill *out for (B, T, d) and a lanes_per_seq request (0 = auto). */
+/* Fill *out for (B, T, d) and a lanes_per_seq request (see Conventions). */
 int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layout* out);
 
 /* ---- host entry points (numpy buffers in, results out) ------------------- */

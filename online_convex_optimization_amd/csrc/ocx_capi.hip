@@ -146,6 +146,22 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     // 1 = exact with auto lanes, -k = exact with k lanes.  Exact mode keeps every sum
     // in the reference's sequential order; with P > 1 the running sum is handed from
     // lane to lane (chain = 1).
+    // OCX_LANES_BEST: the exact-auto layout unless it chains 8+ lanes (d >= 512, or a
+    // few-wave batch), then butterfly sums with at least 4 coordinates per lane: d = 64,
+    // T = 1e5, 3328 sequences measured 69 ms at 16 x 4 (62 % of 8 TB/s) against 75 ms at
+    // 8 x 8, 82 ms at 32 x 2 and 104 ms for the exact 8-lane chain; d = 1024: 52 ms
+    // (81 %) against 102 ms exact (profiles/r02_fewwave_block_shapes.jsonl)
+    bool best_tree = false;
+    if (lanes_per_seq == OCX_LANES_BEST) {
+        ocx_layout Le;
+        if (int rc = ocx_layout_init(B, T, d, 1, &Le)) return rc;
+        if (Le.P < 8) {
+            *L = Le;
+            return OCX_OK;
+        }
+        best_tree = true;
+        lanes_per_seq = 0;
+    }
     const bool exact = (lanes_per_seq == 1 || lanes_per_seq < 0);
     int P = lanes_per_seq < 0 ? -lanes_per_seq : lanes_per_seq;
     // auto: fewest lanes with <= 16 coordinates each (more coordinates per lane cost
@@ -154,7 +170,8 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     int64_t p_min = 1;
     while (p_min < 64 && ceil_div(d, p_min) > 16) p_min *= 2;
     int64_t p_max = 1;
-    while (p_max < 64 && ceil_div(d, p_max * 2) >= 2) p_max *= 2;
+    const int64_t c_min = best_tree ? 4 : 2;  // fewest coordinates per lane
+    while (p_max < 64 && ceil_div(d, p_max * 2) >= c_min) p_max *= 2;
     if (lanes_per_seq == 0) {
         // auto: enough lanes for ~8 wavefronts per CU (131072 lanes on
         // 256 CUs) when B allows.

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -209,8 +209,7 @@ hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt,
                         double* cum_r, double* cum_e, double* comp_e, double* comp_f,
                         double* cmp_out, int* regime, hipStream_t st) {
     hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C, P, false)>),
-                       dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
-                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e,
+                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e,
                        comp_e, comp_f, cmp_out, regime);
     return hipGetLastError();
 }

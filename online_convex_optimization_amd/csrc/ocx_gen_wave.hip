@@ -18,6 +18,7 @@
 // wave): no per-lane rows, so occupancy is set by registers, every lane works on
 // every round, and a batch of a few thousand sequences already fills the GPU.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ocx_internal.h"
 #include "ocx_rng.h"
@@ -42,11 +43,13 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
 __device__ __forceinline__ ocx_u128 rl128(ocx_u128 v, int lane) {
     return ((ocx_u128)rl64((uint64_t)(v >> 64), lane) << 64) | rl64((uint64_t)v, lane);
 }
+// lane k gets lane k+1's value (DPP wave_shl:1, a VALU move; lane 63 keeps its own, which
+// no caller reads: a rejected lane 63 is redrawn next round)
 __device__ __forceinline__ uint64_t shfl_down1(uint64_t v) {
-    const int addr = (int)(((threadIdx.x & 63) + 1) & 63) << 2;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)(uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
+    int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    lo = __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xF, 0xF, false);
+    hi = __builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xF, 0xF, false);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 __device__ __forceinline__ double shfl_double(double v, int src) {
     const int addr = src << 2;
@@ -138,7 +141,11 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const uint64_t rabs = (r8 >> 1) & kMask52;
     double x = u52_to_double(rabs) * tb.wi[idx];
     if (r8 & 1) x = -x;
+#ifdef OCX_GEN_TUNE_NO_PARSE  // tuning only: every draw accepted (wrong normals)
+    const bool fast = true;
+#else
     const bool fast = rabs < tb.ki[idx];
+#endif
     const uint64_t rej = ballot(!fast);
     if (rej == 0 && need == 64) {  // every draw accepted (64 % of rounds)
         if (RING) ring[(head + (unsigned)lane) & rmask] = x;
@@ -151,7 +158,11 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         // wedge test of a rejected draw k uses draw k+1 (next_double) as its uniform
         const uint64_t rn = shfl_down1(r);
         bool wa = false;
+#ifdef OCX_GEN_TUNE_NO_WEDGE  // tuning only: no wedge test (wrong normals)
+        if (false) {
+#else
         if (!fast && idx != 0) {
+#endif
             const double lhs = (tb.fi[idx - 1] - tb.fi[idx]) * u53(rn) + tb.fi[idx];
             const double a = -0.5 * x * x;
             const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
@@ -161,7 +172,15 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         }
         wacc = ballot(wa);
         const uint64_t tailm = ballot(!fast && idx == 0);
+        // Usual case: no tail draw and no two rejected draws side by side, so every
+        // rejected draw k takes draw k+1 as its uniform and a rejected draw 63 is redone
+        // next round: the walk below reduces to two bit operations.
         uint64_t rem = rej;
+        if (tailm == 0 && (rej & (rej << 1)) == 0) {
+            cons = rej << 1;
+            limit = (rej >> 63) ? 63 : 64;
+            rem = 0;
+        }
         while (rem) {
             const int k = __builtin_ctzll(rem);
             rem &= rem - 1;
@@ -307,6 +326,11 @@ __device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, 
 }
 
 constexpr int kWaveBlock = 256;
+#ifdef OCX_GEN_TUNE_NO_STORE  // tuning only: rows computed, not written
+#define OCX_GEN_STORE(v, p) do { if ((v) == 1234.5) *(p) = (v); } while (0)
+#else
+#define OCX_GEN_STORE(v, p) __builtin_nontemporal_store((v), (p))
+#endif
 // Waves per SIMD the register allocation must allow.  For the d = 64 kernel 6 waves
 // (80 VGPRs, a few cold spills) measured 6 % faster than the unconstrained 104 VGPRs
 // (4 waves); its LDS (6 KB tables + 4 x 4 KB rings per block) also admits 6.
@@ -317,9 +341,15 @@ constexpr int kWaveBlock = 256;
 #endif
 
 // rows per batch leaving the ring (see the kernel)
+#ifndef OCX_GEN_ROWS64
+// rows per batch at 32 < d <= 64: 8 rows use all 64 lanes for the 8-accumulator sums of
+// squares and share one sqrt/div sequence (d = 64, 32768 x 1e4: 84.8 ms vs 92.9 at 4 rows,
+// profiles/r02_gen_variants.jsonl)
+#define OCX_GEN_ROWS64 8
+#endif
 __host__ __device__ __forceinline__ int batch_rows(int d) {
     if (d < 8) return 32;
-    if (d <= 128) return d <= 32 ? 8 : (d <= 64 ? 4 : 2);
+    if (d <= 128) return d <= 32 ? 8 : (d <= 64 ? OCX_GEN_ROWS64 : 2);
     return 1;
 }
 constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion depth <= 16
@@ -466,7 +496,11 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
                 const int nrows = ready < R ? ready : R;
                 // this lane's row of the batch and its clip scale
                 double sc = 1.0;
+#ifdef OCX_GEN_TUNE_NO_NORM  // tuning only: no row norms (unclipped rows)
+                if (false) {
+#else
                 if (d <= 128) {
+#endif
                     const int r = d < 8 ? lane : (lane >> 3);
                     const unsigned o = tailp + (unsigned)(r * d);
                     double ss = 0.0;
@@ -490,7 +524,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
                         if (rl == 0) {
                             const double v =
                                 jl < d ? ring[(tailp + (unsigned)(r * d + jl)) & rmask] * scr : 0.0;
-                            __builtin_nontemporal_store(v, zt + zoff + (t + r) * 128);
+                            OCX_GEN_STORE(v, zt + zoff + (t + r) * 128);
                         }
                     }
                 } else if (Dp <= 64 && d <= 128) {
@@ -500,7 +534,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
                         if (rl < RP && r < nrows) {
                             const double v =
                                 jl < d ? ring[(tailp + (unsigned)(r * d + jl)) & rmask] * scr : 0.0;
-                            __builtin_nontemporal_store(v, zt + zoff + (t + r) * 128);
+                            OCX_GEN_STORE(v, zt + zoff + (t + r) * 128);
                         }
                     }
                 } else {
@@ -593,7 +627,14 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF>,
                                                      kWaveBlock, lds);
     if (e != hipSuccess) return e;
-    const int64_t resident = std::max<int64_t>(1, (int64_t)cus * std::max(per_cu, 1) * (kWaveBlock / 64));
+    int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
+    // OCX_GEN_WAVES_PER_SIMD caps the resident generator waves (leaves registers free for
+    // a kernel running beside it on another stream)
+    if (const char* ev = std::getenv("OCX_GEN_WAVES_PER_SIMD")) {
+        const int64_t cap = std::atoll(ev);
+        if (cap > 0) waves_per_cu = std::min<int64_t>(waves_per_cu, 4 * cap);
+    }
+    const int64_t resident = std::max<int64_t>(1, (int64_t)cus * waves_per_cu);
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
     const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));

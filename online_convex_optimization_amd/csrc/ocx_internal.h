@@ -3,11 +3,40 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "../../include/ocx.h"
 
 #define OCX_WAVE 64
 #define OCX_BLOCK 256  // 4 wave-groups per workgroup
 #define OCX_WAVES_PER_BLOCK (OCX_BLOCK / OCX_WAVE)
+
+// Wave-group index of the calling wave: blocks hold blockDim.x / 64 waves (see
+// ocx_block_waves; kernels are compiled for OCX_BLOCK threads and launched with 64,
+// 128 or 256).
+__device__ __forceinline__ int64_t ocx_wave_id() {
+    return (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+
+// Waves per workgroup for a launch of G independent wave-groups.  Four-wave blocks pack a
+// CU's four SIMDs, but a launch of few waves (capacity-limited long horizons, d = 1024)
+// then lands on G/4 CUs and leaves the rest idle: below 8 waves per CU use one-wave
+// blocks, which the dispatcher spreads over every CU.  OCX_BLOCK_WAVES=1|2|4 forces it.
+inline int ocx_block_waves(int64_t G) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char* e = std::getenv("OCX_BLOCK_WAVES");
+        const int v = e ? std::atoi(e) : 0;
+        forced = (v == 1 || v == 2 || v == 4) ? v : 0;
+    }
+    if (forced) return forced;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return G >= 8 * (int64_t)cus ? OCX_WAVES_PER_BLOCK : 1;
+}
+inline dim3 ocx_grid(int64_t G, int wpb) { return dim3((unsigned)((G + wpb - 1) / wpb)); }
 
 // ---------------------------------------------------------------------------
 // Cross-lane fp64 reductions over the P lanes that own one sequence.

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_kernel(
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -434,16 +434,14 @@ __global__ void ocx_max_kernel(const double* __restrict__ r, int64_t B, double* 
 // ---------------------------------------------------------------------------
 namespace {
 
-inline unsigned grid_for(int64_t G) {
-    return (unsigned)((G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK);
-}
+// (grid, block) of a launch over G wave-groups (ocx_block_waves)
+#define OCX_SHAPE(G) ocx_grid((G), ocx_block_waves(G)), dim3(64 * ocx_block_waves(G))
 
 template <int C, int P, bool CH>
 hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int algo,
                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
                          double* xl, double* cmp_out, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), dim3(grid_for(L->G)),
-                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, algo, eta0, cmp,
+    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), OCX_SHAPE(L->G), 0, st, zt, yt, L->B, L->T, L->d, L->G, algo, eta0, cmp,
                        reg, cum, comp, xl, cmp_out, regime);
     return hipGetLastError();
 }
@@ -452,7 +450,7 @@ template <int C, int P, bool CH>
 hipError_t launch_smart_cp(const ocx_layout* L, const double* zt, const double* yt,
                            const double* th, double eta0, double* reg, int64_t* sw,
                            hipStream_t st) {
-    hipLaunchKernelGGL((ocx_smart_kernel<C, P, CH>), dim3(grid_for(L->G)), dim3(OCX_BLOCK), 0, st,
+    hipLaunchKernelGGL((ocx_smart_kernel<C, P, CH>), OCX_SHAPE(L->G), 0, st,
                        zt, yt, L->B, L->T, L->G, th, eta0, reg, sw);
     return hipGetLastError();
 }
@@ -460,7 +458,7 @@ hipError_t launch_smart_cp(const ocx_layout* L, const double* zt, const double* 
 template <int C, int P, bool CH>
 hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double* yt,
                             const double* at, double* cum, double* comp, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_replay_kernel<C, P, CH>), dim3(grid_for(L->G)), dim3(OCX_BLOCK), 0,
+    hipLaunchKernelGGL((ocx_replay_kernel<C, P, CH>), OCX_SHAPE(L->G), 0,
                        st, zt, yt, at, L->B, L->T, L->G, cum, comp);
     return hipGetLastError();
 }
@@ -468,8 +466,7 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
 template <int C, int P, bool CH>
 hipError_t launch_prefix_cp(const ocx_layout* L, const double* zt, const double* yt,
                             double* actions, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_prefix_actions_kernel<C, P, CH>), dim3(grid_for(L->G)),
-                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->d, L->G, actions, regime);
+    hipLaunchKernelGGL((ocx_prefix_actions_kernel<C, P, CH>), OCX_SHAPE(L->G), 0, st, zt, yt, L->B, L->T, L->d, L->G, actions, regime);
     return hipGetLastError();
 }
 

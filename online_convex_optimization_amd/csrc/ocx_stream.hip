@@ -25,7 +25,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * OCX_WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t g = ocx_wave_id();
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
@@ -132,8 +132,7 @@ hipError_t launch_chunk_cp(const ocx_layout* L, const double* zt, const double* 
                            int alg_flag, double eta0, int mode, double* th, double* cum,
                            double* comp, double* reg, hipStream_t st) {
     hipLaunchKernelGGL((ocx_alg_chunk_kernel<C, P, CH, nb_for(C, P)>),
-                       dim3((unsigned)((L->G + OCX_WAVES_PER_BLOCK - 1) / OCX_WAVES_PER_BLOCK)),
-                       dim3(OCX_BLOCK), 0, st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode,
+                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode,
                        th, L->Dp, cum, comp, reg);
     return hipGetLastError();
 }

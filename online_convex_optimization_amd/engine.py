@@ -10,9 +10,14 @@ Two ways in:
   any number of times without touching the host.  Device memory and streams come
   from PyTorch (plumbing only); every kernel is the HIP code in ``csrc/``.
 
-Every call defaults to ``lanes_per_seq=1`` (exact mode: the reference's sequential sums,
-bit-identical results).  ``lanes_per_seq=0`` selects the butterfly layout, faster only
-where exact chains are latency-bound (d in the hundreds and up; ~1e-16 relative).
+Every batched call defaults to ``lanes_per_seq=LANES_BEST`` (include/ocx.h,
+OCX_LANES_BEST): the exact layout — the reference's sequential sums, bit-identical
+results — wherever its lane chains are short and the kernels stream at the HBM roofline
+(e.g. d=64 with >= 8192 sequences per batch, every d <= 16 batch), and butterfly sums
+(~1e-16 relative) where an exact chain of 8+ lanes would leave the kernel latency-bound:
+d >= 512 and few-wave batches (the capacity-limited T=1e5 g(T) batch).
+``lanes_per_seq=1`` forces the bit-exact layout; the drop-in modules (fast_algorithms,
+exact_ftl) always use it.
 """
 from __future__ import annotations
 
@@ -26,6 +31,8 @@ from . import _lib
 from ._lib import ptr
 
 SQRT2 = math.sqrt(2.0)
+LANES_BEST = 128  # OCX_LANES_BEST: exact where it streams at the roofline, butterfly elsewhere
+LANES_EXACT = 1   # bit-identical to the reference's sequential sums
 
 
 def _f64(a) -> np.ndarray:
@@ -42,7 +49,7 @@ def _check_zy(z: np.ndarray, y: np.ndarray):
 
 
 def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=None, *,
-                       lanes_per_seq: int = 1, device: int = 0, return_all: bool = False):
+                       lanes_per_seq: int = LANES_BEST, device: int = 0, return_all: bool = False):
     """fast_algorithms.py:88-115 over B independent sequences on one GPU.
 
     z [B, T, d], y [B, T]; comparator [B, d] optional (exact_ftl.py:266-269).
@@ -66,7 +73,7 @@ def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=
     return reg
 
 
-def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = 1,
+def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = LANES_BEST,
                          device: int = 0, return_switch: bool = False):
     """fast_algorithms.py:118-164 over B sequences; thresh scalar or [B]."""
     z = _f64(z)
@@ -106,7 +113,7 @@ def _reject_out_of_regime(ok: np.ndarray) -> None:
             "y_t = ±1); the general exact-FTL SOCP is out of scope")
 
 
-def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: int = 0,
+def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, device: int = 0,
                     check_regime: bool = True):
     """exact_ftl.py:280-333 (compute_prefix_actions + replay) for B sequences on the GPU,
     in the closed form that is the exact SOCP solution when every ||z_t|| <= 1 and
@@ -133,7 +140,7 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: i
     return cum, comp, act, ok
 
 
-def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, device: int = 0,
+def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, device: int = 0,
                              check_regime: bool = True):
     """exact_ftl.py:280-303 compute_prefix_actions for B sequences on the GPU
     (include/ocx.h, ocx_ftl_prefix_actions_batch): actions [B, T+1, d] with actions[:, t]
@@ -156,7 +163,7 @@ def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = 1, 
     return act, ok
 
 
-def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, device: int = 0,
+def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = LANES_BEST, device: int = 0,
                         check_regime: bool = True, with_ftl_comparator: bool = False):
     """exact_ftl_driver.py:157-186 for B sequences in one read of the data: exact FTL
     (closed form, as ftl_exact_batch) and FTRL against its comparator actions[T].
@@ -185,7 +192,7 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = 1, de
 
 
 def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
-               run0: int = 0, lanes_per_seq: int = 1, device: int = 0) -> np.ndarray:
+               run0: int = 0, lanes_per_seq: int = LANES_BEST, device: int = 0) -> np.ndarray:
     """Regrets of FTRL on _rng(base_seed, T, run) sequences, run in [run0, run0+runs),
     generated on device (fast_algorithms.py:230-241 with a ``d`` parameter)."""
     if base_seed < 0 or base_seed >= 2 ** 64:
@@ -211,7 +218,7 @@ def max_regret(regrets: np.ndarray) -> float:
 
 def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
              eta0: float = SQRT2, devices: Optional[Sequence[int]] = None,
-             lanes_per_seq: int = 1) -> dict:
+             lanes_per_seq: int = LANES_BEST) -> dict:
     """empirical_worst_case_thresholds on one or several GPUs of this process.
 
     Runs are split into contiguous shards, one per device, each generated and
@@ -251,7 +258,7 @@ class DeviceBatch:
     of this object is launched on it, so torch events recorded on that stream
     bracket the HIP kernels exactly."""
 
-    def __init__(self, B: int, T: int, d: int, *, lanes_per_seq: int = 1, device: int = 0,
+    def __init__(self, B: int, T: int, d: int, *, lanes_per_seq: int = LANES_BEST, device: int = 0,
                  stream=None):
         import torch
         self.torch = torch

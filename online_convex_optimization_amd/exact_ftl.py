@@ -85,7 +85,8 @@ class ExactFTLNoClip:
     def _solve_length(self, z_src: np.ndarray, y_src: np.ndarray, length: int) -> np.ndarray:
         """Exact FTL solution of the first ``length`` rows (GPU, closed form)."""
         _, _, act, _ = _engine.ftl_exact_batch(z_src[None, :length], y_src[None, :length],
-                                               norm=self.norm, device=_fa._DEVICE)
+                                               norm=self.norm, lanes_per_seq=_fa.EXACT,
+                                               device=_fa._DEVICE)
         return act[0]
 
     def _solve_current(self) -> np.ndarray:
@@ -163,6 +164,7 @@ def compute_prefix_actions(solver, z: np.ndarray, y: np.ndarray) -> np.ndarray:
         raise ValueError("Solver T_max is smaller than sequence length")
     if isinstance(solver, ExactFTLNoClip):
         actions, _ = _engine.ftl_prefix_actions_batch(z_arr[None], y_arr[None], norm=solver.norm,
+                                                      lanes_per_seq=_fa.EXACT,
                                                       device=_fa._DEVICE)
         solver._set_prefix(z_arr, y_arr, T)
         return actions[0]
@@ -222,7 +224,7 @@ def _ftl_exact_gpu(z_arr, y_arr, norm) -> RunResult:
     if norm not in _NORMS:
         raise ValueError("norm must be one of {'l2','linf','l1'}")
     cum, comp, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
-                                                device=_fa._DEVICE)
+                                                lanes_per_seq=_fa.EXACT, device=_fa._DEVICE)
     return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - comp[0]),
                      comp_loss=float(comp[0]), x_last=act[0].copy())
 

@@ -48,12 +48,14 @@ def max_regret(regrets) -> float:
 
 def gT_sweep_distributed(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
                          compute: Callable[[int, int, int], np.ndarray] = None,
-                         device=None) -> Dict[int, Tuple[float, np.ndarray]]:
+                         device=None, lanes_per_seq: int = 128
+                         ) -> Dict[int, Tuple[float, np.ndarray]]:
     """empirical_worst_case_thresholds across the ranks of the default process group.
 
     ``compute(T, run0, count)`` returns this rank's regrets (default: regenerate and
     simulate on the local GPU through engine.gT_regrets).  ``device`` is where the gather
     runs: the rank's current GPU under the "nccl" (RCCL) backend, host memory otherwise.
+    ``lanes_per_seq`` as engine.gT_regrets (default OCX_LANES_BEST; 1 = bit-exact).
     Returns, on every rank, {T: (g(T), regrets[runs] in run order)}."""
     import torch
     import torch.distributed as dist
@@ -67,7 +69,7 @@ def gT_sweep_distributed(T_grid: Sequence[int], runs: int, *, base_seed: int = 0
 
         def compute(T, run0, count):
             return engine.gT_regrets(T, count, base_seed=base_seed, d=d, run0=run0,
-                                     device=dev_index)
+                                     lanes_per_seq=lanes_per_seq, device=dev_index)
     out = {}
     for T in T_grid:
         T = int(T)

@@ -2,9 +2,10 @@
 
 Same names, signatures and outputs (float32 arrays, NumPy streams via ``_rng``) as
 the reference module, so ``fast_driver.py``-style code can import either.  These
-build inputs on the host; the g(T) adversary has an on-device generator
-(``engine.DeviceBatch.generate_gT``), the four families below get theirs in a later
-round.
+build one sequence at a time on the host, as the reference does.  The batched drivers
+do not use them: the g(T) adversary (``engine.DeviceBatch.generate_gT``) and the four
+families below (``engine.DeviceBatch.generate_family``, ``ocx_dev_gen_family``) are
+generated on device, bit-identical to these builders (tests/test_gpu_parity.py).
 """
 from __future__ import annotations
 

@@ -76,6 +76,26 @@ def test_auto_layout_choices():
     assert _lib.layout(3, 10, 12, -2).C == 8                # chain C is a power of two
 
 
+def test_best_layout_choices():
+    """OCX_LANES_BEST (128): the exact layout while its chains stay under 8 lanes, else
+    butterfly sums with at least 4 coordinates per lane."""
+    best = 128
+    L = _lib.layout(32768, 10, 64, best)       # the bench batch: exact, 4-lane chain
+    assert (L.P, L.C, L.chain) == (4, 16, 1)
+    L = _lib.layout(65536, 10, 16, best)       # configs[1]: exact, one lane per sequence
+    assert (L.P, L.chain) == (1, 0)
+    L = _lib.layout(768, 10, 5, best)          # the drivers' batches: exact
+    assert (L.P, L.C, L.chain) == (4, 2, 1)
+    L = _lib.layout(4900, 10, 64, best)        # few-wave (T = 1e5 batch): butterfly 16 x 4
+    assert (L.P, L.C, L.chain) == (16, 4, 0)
+    L = _lib.layout(3328, 10, 64, best)
+    assert (L.P, L.C, L.chain) == (16, 4, 0)
+    L = _lib.layout(2048, 10, 1024, best)      # configs[4]: butterfly 64 x 16
+    assert (L.P, L.C, L.chain) == (64, 16, 0)
+    L = _lib.layout(1, 10, 3, best)            # a single short sequence: exact
+    assert L.P * L.C >= 3 and (L.P == 1 or L.chain == 1)
+
+
 def test_untile_roundtrip_matches_pack_formula():
     # host restatement of ocx_pack_z_kernel's plane-major index map, inverted by untile_z
     B, T, d = 37, 5, 11

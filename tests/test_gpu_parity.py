@@ -332,6 +332,26 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
             assert chunked[r] == ref
 
 
+@pytest.mark.parametrize("T,d,runs,exact", [(200, 64, 700, False), (60, 64, 9000, True),
+                                             (40, 1024, 40, False), (300, 5, 500, True)])
+def test_best_mode_default(ocx, T, d, runs, exact):
+    """The batched APIs' default (OCX_LANES_BEST): the exact layout (bit-identical) where
+    its chains are short — d=64 with >= 8192 sequences, small d — and butterfly sums
+    (<= 1e-12 relative) for few-wave d=64 batches and d=1024."""
+    eng, lib = ocx["engine"], ocx["lib"]
+    L = lib.layout(runs, T, d, eng.LANES_BEST)
+    assert bool(L.P == 1 or L.chain) == exact
+    reg = eng.gT_regrets(T, runs, base_seed=9, d=d)
+    assert np.array_equal(reg, eng.gT_regrets(T, runs, base_seed=9, d=d,
+                                              lanes_per_seq=eng.LANES_BEST))
+    for r in (0, runs // 3, runs - 1):
+        z, y = O.gT_sample(9, T, r, d)
+        ref = O.simulate_alg(z, y, 0, SQ2)
+        assert reg[r] == ref if exact else close(reg[r], ref), (r, reg[r], ref)
+    if exact:
+        assert np.array_equal(reg, eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=1))
+
+
 @pytest.mark.parametrize("P", [1, 0])
 def test_streamed_gT_ragged_last_batch(ocx, monkeypatch, P):
     """More runs than one streamed batch (131 072) with a short last batch: the last batch

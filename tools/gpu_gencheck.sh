@@ -1,0 +1,9 @@
+#!/bin/bash
+# Generator timing + the parity tests that exercise it (NumPy stream equality, g(T) curves).
+set -u
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; mkdir -p gpurun_out
+timeout -k 10 300 python tools/tune_gen.py --rounds 3 > gpurun_out/tune_gen5.jsonl || exit 2
+cut -c1-200 gpurun_out/tune_gen5.jsonl
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 3; }
+tail -1 gpurun_out/pytest_gpu.log

@@ -63,13 +63,14 @@ def gen1(args):
 def sweep(args):
     from online_convex_optimization_amd import engine
     for T, runs in ((100, 1000000), (1000, 1000000), (10000, 131072), (100000, 131072)):
-        engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)  # warm (incl. the HBM buffers)
+        engine.gT_regrets(T, runs, d=64, lanes_per_seq=args.lanes)  # warm (incl. HBM buffers)
         t0 = time.perf_counter()
-        regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=1)
+        regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=args.lanes)
         dt = time.perf_counter() - t0
-        print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64, "seconds": dt,
-                          "timesteps_per_s": T * runs / dt, "g": engine.max_regret(regs)}),
-              flush=True)
+        print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64, "lanes": args.lanes,
+                          "seconds": dt, "timesteps_per_s": T * runs / dt,
+                          "frac_1040B": T * runs / dt * 1040 / 8e12,
+                          "g": engine.max_regret(regs)}), flush=True)
 
 
 def driver(args):
@@ -139,8 +140,7 @@ def config4(args):
     exact and butterfly sums, at two HBM budgets (resident vs streamed batches)."""
     from online_convex_optimization_amd import engine
     T, d = 10000, 1024
-    cases = [(8192, 0, None, None), (8192, 1, None, None), (32768, 0, None, None),
-             (8192, 0, "64", "8192"), (8192, 1, "64", "8192")]
+    cases = [(8192, 128, None, None), (8192, 1, None, None), (32768, 128, None, None)]
     for runs, lanes, budget, minres in cases:
         if budget:
             os.environ["OCX_HBM_BUDGET_GB"] = budget
@@ -240,6 +240,7 @@ def smart(args):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
+    ap.add_argument("--lanes", type=int, default=128, help="lanes_per_seq of the sweeps")
     ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget", "prof_long"])
     a = ap.parse_args()
     for w in a.what:
