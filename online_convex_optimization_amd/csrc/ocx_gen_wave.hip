@@ -241,7 +241,17 @@ __device__ __forceinline__ double leaf_sumsq(const double* ring, int rmask, unsi
         const int n8 = n - (n % 8);
         const unsigned ok = o + (unsigned)(lane & 7);
         double acc;
-        if constexpr (NF >= 8) {
+        if constexpr (NF == 64) {
+            // rows of 64 start at multiples of 64 in a ring of a multiple of 64: a row
+            // never wraps, so one masked base and immediate offsets (ds_read2_b64 pairs)
+            const double* rp = ring + (o & (unsigned)rmask) + (lane & 7);
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = rp[8 * q];
+            acc = v[0] * v[0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) acc += v[q] * v[q];
+        } else if constexpr (NF >= 8) {
             constexpr int M = (NF - NF % 8) / 8;
             double v[M];
 #pragma unroll
@@ -516,7 +526,18 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
                     sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
                 }
                 const int sc_stride = d < 8 ? 1 : 8;
-                if (Dp <= 64 && d <= 128 && RP == 1) {
+                if (DF == 64) {
+                    // whole rows of 64, never wrapping (see leaf_sumsq): lane j stores
+                    // coordinate j of each row, at immediate LDS offsets from one base
+                    const double* rp = ring + (tailp & (unsigned)rmask) + lane;
+                    double* zp = zt + zoff + t * 128;
+                    for (int r = 0; r < nrows; ++r) {
+                        const double scr = __hiloint2double(
+                            __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
+                            __builtin_amdgcn_readlane(__double2loint(sc), r * sc_stride));
+                        OCX_GEN_STORE(rp[64 * r] * scr, zp + r * 128);
+                    }
+                } else if (Dp <= 64 && d <= 128 && RP == 1) {
                     for (int r = 0; r < nrows; ++r) {
                         const double scr = __hiloint2double(
                             __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
