@@ -3,9 +3,13 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
 
-A step = one launch of the FTRL kernel (main T-step loop + comparator pass) over
+A step = one launch of the FTRL kernel (main T-step loop + comparator loss) over
 one resident batch of B sequences per GPU (default B = 32768: a 168 GB resident
-chunk of configs[2]'s 1e5-trial job).  Inputs are the reference's g(T) adversary
+chunk of configs[2]'s 1e5-trial job).  By default the comparator loss of FTL(theta_T)
+takes its closed form T/2 - ||theta_T|| (valid for the sampler's clipped rows and +-1
+labels, certified per sequence by the kernel; include/ocx.h OCX_ALG_CLIPPED_ROWS), so
+the kernel reads z once; ``--comparator two-pass`` streams z a second time as the
+reference does, and the line reports that kernel beside the default as ``two_pass``.  Inputs are the reference's g(T) adversary
 (_rng(0, T, run) streams, fast_algorithms.py:231-239, d = 64) generated ON DEVICE
 before the timed region.  Each rank simulates its own runs (weak scaling, no
 data-path collective); each step ends with one all-gather of the regrets to
@@ -13,7 +17,8 @@ collect the regret vector (the only exchange the path has).
 
 Printed (rank 0, one JSON line): value = all ranks' timesteps / max-over-ranks
 time; roofline of the kernel from HIP events on its stream (algorithmic bytes =
-2·(8d+8) per timestep); cpu_baseline = oracle/ocx_oracle.c (C port of
+(8d+8) per timestep per pass over z: one pass with the closed-form comparator, two
+with the streamed one); cpu_baseline = oracle/ocx_oracle.c (C port of
 _simulate_alg_core) single-threaded on a bounded sample of the same sequences; the
 parity error of the GPU regrets against that CPU sample.
 """
@@ -48,6 +53,14 @@ def parse():
                          "layout where it streams at the roofline, butterfly sums where exact "
                          "chains are latency-bound), 1 = exact mode (bit-identical to the "
                          "reference, auto lanes), 0 = auto with butterfly sums, k / -k explicit")
+    ap.add_argument("--comparator", choices=("closed", "two-pass"), default="closed",
+                    help="closed: comparator loss T/2 - ||theta_T|| where the kernel certifies "
+                         "it (one pass over z; not in exact lanes mode); two-pass: the "
+                         "reference's second streaming pass")
+    ap.add_argument("--two-pass-steps", type=int, default=3,
+                    help="launches of the two-pass kernel timed after the metric for the "
+                         "two_pass comparison (0 disables; profile runs use 0 so every "
+                         "ocx_alg_kernel launch in the trace is the default one)")
     ap.add_argument("--e2e-steps", type=int, default=3,
                     help="untimed-for-the-metric batches of generation + simulation reported "
                          "as end_to_end (0 disables)")
@@ -151,11 +164,16 @@ def main():
         src = db.regret[:B] if gdev == dev else db.regret[:B].cpu()
         dist.all_gather_into_tensor(gathered, src)
 
-    def step():
-        db.simulate_alg(0, math.sqrt(2))
+    closed = a.comparator == "closed" and not db.exact
+
+    def step(flags=None):
+        db.simulate_alg(0, math.sqrt(2), closed_comparator=closed, closed_out=flags)
         if dist_on:
             gather()
 
+    # which sequences took the closed form (the rest streamed z a second time)
+    flags = torch.zeros(B, dtype=torch.int32, device=dev)
+    step(flags)
     for _ in range(a.warmup):
         step()
     if dist_on:
@@ -166,7 +184,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         ev[i][0].record(stream)
-        db.simulate_alg(0, math.sqrt(2))
+        db.simulate_alg(0, math.sqrt(2), closed_comparator=closed)
         ev[i][1].record(stream)
         if dist_on:
             gather()
@@ -179,6 +197,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    # sequences in waves that streamed the second pass (a wave holds S sequences)
+    fl = np.ones(db.L.G * db.L.S, dtype=np.int32)
+    fl[:B] = flags.cpu().numpy() if closed else 0
+    seq_pass2 = int((fl.reshape(db.L.G, db.L.S).min(axis=1) == 0).sum()) * db.L.S
+    seq_pass2 = min(seq_pass2, B)
+
+    # the same kernel with the reference's second streaming pass, for comparison
+    two_pass = None
+    if closed and a.two_pass_steps > 0:
+        ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(a.two_pass_steps + 1)]
+        for s2, e2 in ev2:
+            s2.record(stream)
+            db.simulate_alg(0, math.sqrt(2), closed_comparator=False)
+            e2.record(stream)
+        torch.cuda.synchronize()
+        ms2 = float(np.mean([s2.elapsed_time(e2) for s2, e2 in ev2[1:]]))
+        b2 = B * T * 2 * (8 * d + 8)
+        two_pass = {"kernel_ms": ms2, "timesteps_per_s_per_gpu": B * T / (ms2 * 1e-3),
+                    "achieved_GBps": b2 / (ms2 * 1e-3) / 1e9,
+                    "frac": b2 / (ms2 * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                    "alg_bytes_per_launch": b2}
+        db.simulate_alg(0, math.sqrt(2), closed_comparator=closed)  # regrets of the default
 
     # End to end (outside the metric's timed region): regenerate the batch on device and
     # simulate it, a.e2e_steps times — what a g(T) sweep / configs[2] job does per batch.
@@ -194,7 +235,7 @@ def main():
             eg[i][0].record(stream)
             db.generate_gT(base_seed=0, run0=run0)
             eg[i][1].record(stream)
-            db.simulate_alg(0, math.sqrt(2))
+            db.simulate_alg(0, math.sqrt(2), closed_comparator=closed)
             eg[i][2].record(stream)
         torch.cuda.synchronize()
         e2e_s = time.perf_counter() - te0
@@ -209,21 +250,25 @@ def main():
                "ms_per_batch": e2e_s / a.e2e_steps * 1e3,
                "gen_kernel_ms": gen_ms, "sim_kernel_ms": sim_ms,
                "roofline_frac": rate / world * 2 * (8 * d + 8) / (PEAK_HBM_GBS * 1e9),
-               "note": "generation (ocx_dev_gen_gT) + FTRL per resident batch; frac counts the "
-                       "FTRL kernel's 2*(8d+8) B/timestep only"}
+               "note": "generation (ocx_dev_gen_gT) + FTRL per resident batch; frac counts "
+                       "2*(8d+8) B/timestep (with the closed-form comparator that is exactly "
+                       "the pipeline's traffic: the generator's write and one FTRL read)"}
 
     regrets = db.regret[:B].cpu().numpy()
     out = None
     if rank == 0:
         steps_per_launch = B * T
         value = world * B * T * a.steps / elapsed
-        alg_bytes = steps_per_launch * 2 * (8 * d + 8)
+        # one pass over z per sequence, a second one for the waves that streamed it
+        alg_bytes = (B + seq_pass2) * T * (8 * d + 8)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         try:
             with open(a.traffic) as f:
                 tr = json.load(f)
-            if (tr.get("B"), tr.get("T"), tr.get("d"), tr.get("P")) == (B, T, d, db.L.P):
+            want = "closed" if closed else "two-pass"
+            if ((tr.get("B"), tr.get("T"), tr.get("d"), tr.get("P")) == (B, T, d, db.L.P)
+                    and tr.get("comparator", "two-pass") == want):
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -232,9 +277,14 @@ def main():
         if a.cpu_seconds > 0:
             cregs, cps, spent = cpu_baseline(T, d, B, a.cpu_seconds)
             err = np.abs(regrets[:len(cregs)] - cregs)
+            # the closed-form comparator differs from the reference's sequential sum by
+            # that sum's own rounding (tests/test_gpu_parity.py close_closed)
+            tol = np.maximum(1e-12 * np.maximum(1.0, np.abs(cregs)), 4 * 2.22e-16 * T ** 1.5)
             parity = {"n_checked": int(len(cregs)), "max_abs_err": float(err.max()),
                       "max_rel_err": float((err / np.maximum(np.abs(cregs), 1e-300)).max()),
-                      "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs))}
+                      "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs)),
+                      "within_tolerance": bool(np.all(err <= tol)),
+                      "tolerance": "max(1e-12*max(1,|ref|), 4*eps*T^1.5); north star 1e-6 rel"}
             acps, threads, nseq, aspent = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 4))
             hc = host_cpu()
             cpu = {"value": cps, "unit": "timesteps/s", "cores": 1, "kind": "port",
@@ -267,6 +317,9 @@ def main():
                        "lanes_mode": {128: "best", 1: "exact", 0: "auto"}.get(a.lanes, str(a.lanes)),
                        "sums": "exact (sequential order)" if (db.L.P == 1 or db.L.chain)
                                else "butterfly",
+                       "comparator": "closed form T/2-||theta_T|| (certified per sequence)"
+                                     if closed else "two-pass (sequential sum)",
+                       "sequences_second_pass": seq_pass2,
                        "parallelism": f"dp{world}",
                        "z_bytes_per_gpu": db.z_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
@@ -275,6 +328,7 @@ def main():
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "parity": parity,
+            "two_pass": two_pass,
             "end_to_end": e2e,
             "gen_seconds": gen_s,
             "gen_timesteps_per_s": B * T / gen_s,

@@ -150,6 +150,22 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
  * returns the R regrets (host array).  Only the regrets leave the GPU. */
 int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
                    double eta0, double* regrets, int lanes_per_seq, int device);
+/* In the bit-exact modes (lanes_per_seq 1 or -k) the comparator pass is the reference's
+ * sequential sum; in the others the clipped-row closed form of ocx_dev_simulate_alg_ex
+ * applies (the sampler's rows satisfy it by construction). */
+
+/* fast_algorithms.py:211-247 empirical_worst_case_thresholds with `d` coordinates, over
+ * several GPUs of this process: for every T of T_grid [nT], the runs [0, runs) are split
+ * into contiguous shards, one per device, each generated and simulated on its own GPU by a
+ * host thread (ocx_gT_regrets).  gmax [nT] = max(0.0, max over runs) as :228,:242-243;
+ * regrets [nT][runs] (nullable) in run order.  ngpus <= 0: every visible device. */
+int ocx_gT_sweep(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed, int64_t d,
+                 double eta0, int ngpus, double* gmax, double* regrets);
+/* ocx_gT_sweep over an explicit device list (a device may repeat: its shards then share
+ * that device's stream) and a lanes_per_seq mode. */
+int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed,
+                         int64_t d, double eta0, const int* devices, int ndev, int lanes_per_seq,
+                         double* gmax, double* regrets);
 
 /* ---- device entry points (tiled layout, caller-owned device memory) ------ */
 
@@ -180,6 +196,24 @@ int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seed
 int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                          int alg_flag, double eta0, const double* comparator, double* regret,
                          double* cum_loss, double* comp_loss, double* x_last, void* stream);
+
+/* ocx_dev_simulate_alg with options.  flags (bitwise or):
+ *   OCX_ALG_CLIPPED_ROWS  the caller asserts ||z_t|| <= 1 for every row (up to rounding),
+ *     as the g(T) sampler's clipped rows (fast_algorithms.py:234-237, ocx_dev_gen_gT) are.
+ *     With comparator == NULL, the loss of FTL(theta_T) over the sequence is then
+ *     T/2 - ||theta_T|| whenever every step's sub-gradient was -y_t/2 (y_t = +-1, no exact
+ *     tie; the kernel checks this per sequence), because |z_t.x* - y_t| = 1 - y_t z_t.x*
+ *     on the unit ball and theta_T = -S_T/2.  A wave whose sequences all pass skips the
+ *     second pass over z: one HBM pass instead of two.  The comparator loss then equals
+ *     the reference's sequential sum up to that sum's rounding (about 1e-12 relative on
+ *     the regret at T = 1e4; the loop itself keeps the layout's summation order); a
+ *     sequence failing the check gets the streamed second pass, bit-identical to flags 0.
+ * closed_out [B] (int32, nullable): 1 where the closed form was taken. */
+#define OCX_ALG_CLIPPED_ROWS 1
+int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                            int alg_flag, double eta0, const double* comparator, double* regret,
+                            double* cum_loss, double* comp_loss, double* x_last, int flags,
+                            int32_t* closed_out, void* stream);
 
 /* ocx_ftl_exact_batch on device (norm 0 = l2 only). */
 int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,

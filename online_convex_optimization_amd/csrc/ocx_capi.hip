@@ -9,6 +9,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ocx.h"
@@ -274,6 +275,19 @@ int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const doubl
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag != 0 ? 1 : 0, eta0, comparator, regret,
                            cum_loss, comp_loss, x_last, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                            int alg_flag, double eta0, const double* comparator, double* regret,
+                            double* cum_loss, double* comp_loss, double* x_last, int flags,
+                            int32_t* closed_out, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (flags & ~OCX_ALG_CLIPPED_ROWS) return fail(OCX_E_INVALID, "unknown flags");
+    OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag != 0 ? 1 : 0, eta0, comparator, regret,
+                           cum_loss, comp_loss, x_last, (hipStream_t)stream, nullptr, closed_out,
+                           (flags & OCX_ALG_CLIPPED_ROWS) ? 1 : 0));
     return OCX_OK;
 }
 
@@ -576,6 +590,9 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
     if (R == 0) return OCX_OK;
     if (!regrets) return fail(OCX_E_INVALID, "NULL regrets");
+    // the sampler's rows are clipped: outside the bit-exact modes the comparator loss
+    // takes the closed form (ocx_dev_simulate_alg_ex), one HBM pass instead of two
+    const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
     DevCtx* cx;
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);
@@ -642,7 +659,8 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
             OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
                                       cx->yt.as<double>(), st));
             OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
-                                   cx->out.as<double>(), nullptr, nullptr, nullptr, st));
+                                   cx->out.as<double>(), nullptr, nullptr, nullptr, st, nullptr,
+                                   nullptr, onepass));
             OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8,
                                    hipMemcpyDeviceToHost, st));
             OCX_HIP(hipStreamSynchronize(st));
@@ -663,7 +681,7 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     ocx_layout Ltail;
     if (int rc = ocx_layout_init(R % Bc ? R % Bc : Bc, 1, d, lanes_per_seq, &Ltail)) return rc;
     OCX_HIP(cx->theta.ensure((size_t)std::max(Bc * L1.Dp, Ltail.B * Ltail.Dp) * 8));
-    OCX_HIP(cx->acc.ensure((size_t)Bc * 3 * 8));
+    OCX_HIP(cx->acc.ensure((size_t)(Bc * 4 + 1) * 8));
     for (int64_t r0 = 0; r0 < R; r0 += Bc) {
         const int64_t nb = std::min(Bc, R - r0);
         ocx_layout Lb;
@@ -674,10 +692,22 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
         double* cum = cx->acc.as<double>();
         double* comp = cum + Bc;
         double* reg = comp + Bc;
+        double* unclean = onepass ? reg + Bc : nullptr;  // [nb + 1]
         OCX_HIP(ocx_launch_gen_seek(base_seed, T, run0 + r0, nb, d, rs, ls, st));
         OCX_HIP(hipMemsetAsync(th, 0, (size_t)nb * Lb.Dp * 8, st));
         OCX_HIP(hipMemsetAsync(cum, 0, (size_t)Bc * 2 * 8, st));
+        if (unclean) OCX_HIP(hipMemsetAsync(unclean, 0, (size_t)(nb + 1) * 8, st));
         for (int pass = 0; pass < 2; ++pass) {
+            if (pass == 1 && unclean) {
+                // closed-form comparator for the clean sequences (no regeneration); the
+                // second pass only when a sequence needs it
+                OCX_HIP(ocx_launch_alg_chunk(&Lb, nullptr, nullptr, T, 0, eta0, 2, th, cum, comp,
+                                             reg, st, unclean));
+                double any = 0.0;
+                OCX_HIP(hipMemcpyAsync(&any, unclean + nb, 8, hipMemcpyDeviceToHost, st));
+                OCX_HIP(hipStreamSynchronize(st));
+                if (any == 0.0) break;
+            }
             for (int64_t c = 0; c < nch; ++c) {
                 const int64_t t0 = c * Tc, tl = std::min(Tc, T - t0);
                 ocx_layout L;
@@ -691,13 +721,61 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
                                                 cx->zt.as<double>(), cx->yt.as<double>(), st));
                 OCX_HIP(ocx_launch_alg_chunk(&L, cx->zt.as<double>(), cx->yt.as<double>(), t0, 0,
                                              eta0, pass, th, cum, comp,
-                                             (pass == 1 && c == nch - 1) ? reg : nullptr, st));
+                                             (pass == 1 && c == nch - 1) ? reg : nullptr, st,
+                                             unclean));
             }
         }
         OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
         OCX_HIP(hipStreamSynchronize(st));
     }
     return OCX_OK;
+}
+
+int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed,
+                         int64_t d, double eta0, const int* devices, int ndev, int lanes_per_seq,
+                         double* gmax, double* regrets) {
+    if (nT < 0 || runs < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
+    if (nT == 0) return OCX_OK;
+    if (!T_grid || !gmax || !devices || ndev < 1) return fail(OCX_E_INVALID, "NULL argument");
+    for (int i = 0; i < nT; ++i)
+        if (T_grid[i] < 0) return fail(OCX_E_INVALID, "negative T");
+    std::vector<double> tmp(regrets ? 0 : (size_t)runs);
+    for (int i = 0; i < nT; ++i) {
+        double* row = regrets ? regrets + (size_t)i * runs : tmp.data();
+        // contiguous shards [runs*k/ndev, runs*(k+1)/ndev), one host thread per shard
+        std::vector<int> rc(ndev, OCX_OK);
+        std::vector<std::string> err(ndev);
+        auto work = [&](int k) {
+            const int64_t lo = runs * k / ndev, hi = runs * (k + 1) / ndev;
+            rc[k] = ocx_gT_regrets(base_seed, T_grid[i], lo, hi - lo, d, eta0, row + lo,
+                                   lanes_per_seq, devices[k]);
+            if (rc[k]) err[k] = g_err;  // the message is thread-local
+        };
+        std::vector<std::thread> th;
+        for (int k = 1; k < ndev; ++k) th.emplace_back(work, k);
+        work(0);
+        for (auto& t : th) t.join();
+        for (int k = 0; k < ndev; ++k)
+            if (rc[k]) return fail(rc[k], "device " + std::to_string(devices[k]) + ": " + err[k]);
+        double m = 0.0;  // fast_algorithms.py:228, :242-243
+        for (int64_t r = 0; r < runs; ++r)
+            if (row[r] > m) m = row[r];
+        gmax[i] = m;
+    }
+    return OCX_OK;
+}
+
+int ocx_gT_sweep(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed, int64_t d,
+                 double eta0, int ngpus, double* gmax, double* regrets) {
+    int n = 0;
+    OCX_HIP(hipGetDeviceCount(&n));
+    if (ngpus <= 0) ngpus = n;
+    if (ngpus > n) return fail(OCX_E_INVALID, "ngpus " + std::to_string(ngpus) +
+                                                  " > device count " + std::to_string(n));
+    std::vector<int> devs(ngpus);
+    for (int k = 0; k < ngpus; ++k) devs[k] = k;
+    return ocx_gT_sweep_devices(T_grid, nT, runs, base_seed, d, eta0, devs.data(), ngpus,
+                                OCX_LANES_BEST, gmax, regrets);
 }
 
 }  // extern "C"

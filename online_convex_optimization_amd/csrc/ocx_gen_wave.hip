@@ -645,6 +645,11 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
+    // OCX_GEN_CUS: CUs the launch may use (a stream restricted to a CU mask)
+    if (const char* ev = std::getenv("OCX_GEN_CUS")) {
+        const int n = std::atoi(ev);
+        if (n > 0 && n < cus) cus = n;
+    }
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF>,
                                                      kWaveBlock, lds);
     if (e != hipSuccess) return e;

@@ -43,12 +43,16 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t d, int64_t G, int algo, double eta0, const double* __restrict__ comparator,
     double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
-    double* __restrict__ x_last, double* __restrict__ cmp_out, int* __restrict__ regime_out) {
+    double* __restrict__ x_last, double* __restrict__ cmp_out, int* __restrict__ regime_out,
+    int onepass) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
     const int64_t g = ocx_wave_id();
     if (g >= G) return;
+#ifdef OCX_ALG_PRIO  // tuning: issue priority over waves of a kernel running beside it
+    __builtin_amdgcn_s_setprio(OCX_ALG_PRIO);
+#endif
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
@@ -59,6 +63,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     const bool ftl = (algo != 0);
     const bool exact = (algo == 2);
     bool linear = true;  // algo 2: data inside the closed form's regime so far
+    bool clean = true;   // onepass: every sub-gradient so far was −y_t/2 (see below)
 
     double th[C];
 #pragma unroll
@@ -111,6 +116,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 const double diff = q - yb[u];  // :106-111
                 cum += 0.5 * fabs(diff);
                 double gq = ocx_grad(diff);
+                clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
                 if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
                     double p[C];
 #pragma unroll
@@ -125,9 +131,25 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         }
     }
 
+    // ---- closed-form comparator (onepass) ----
+    // For rows with ||z_t|| <= 1 (the g(T) sampler's clipped rows: the caller asserts it)
+    // and x* = FTL(theta_T) in the unit ball, |z_t.x* − y_t| = 1 − y_t z_t.x* when y_t = ±1,
+    // so the comparator loss is ½(T − x*.S_T), S_T = Σ y_t z_t.  If every step's
+    // sub-gradient was −y_t/2 (no tie, y_t = ±1: `clean`), theta_T = −½ S_T exactly
+    // (powers of two), x* = −theta/||theta|| and the loss is T/2 − ||theta_T||: no second
+    // pass over z.  It equals the reference's sequential sum up to rounding (≈1e-13
+    // relative on the regret, tests/test_gpu_parity.py).  A wave with an unclean
+    // sequence streams the second pass for it; every clean sequence keeps the closed
+    // form, so a sequence's result never depends on the wave it shares.
+    const bool closed = onepass && comparator == nullptr && !exact && (clean || b >= B);
+    const bool pass2 = __ballot(!closed) != 0;  // wave-uniform
+
     // ---- comparator action (fast_algorithms.py:113 FTL of theta, or the caller's) ----
     double xs[C];
-    if (comparator != nullptr) {
+    if (!pass2 && cmp_out == nullptr) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) xs[j] = 0.0;
+    } else if (comparator != nullptr) {
 #pragma unroll
         for (int j = 0; j < C; ++j) {
             const int64_t jj = (int64_t)c * C + j;
@@ -150,7 +172,8 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     if (true) {
     } else
 #endif
-    if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
+    if (!pass2) {
+    } else if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
         comp = ocx_comp_pass2<C, P, CHAIN, (C <= 8 ? OCX_NB_PASS2 : 4)>(zp, yp, T, kst, S, xs, 0.0, lane);
     } else {
 #pragma unroll
@@ -179,12 +202,21 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         }
         comp = ocx_comp_lane_value<P, CHAIN>(comp, lane);
     }
+    if (__ballot(closed) != 0) {  // wave-uniform: the sum below crosses lanes
+        double p[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+        const double nrm = sqrt(ocx_total<C, P, CHAIN>(p, lane));
+        if (closed) comp = 0.5 * (double)T - nrm;
+    }
 
     if (c == 0 && b < B) {
         if (regret) regret[b] = cum - comp;
         if (cum_out) cum_out[b] = cum;
         if (comp_out) comp_out[b] = comp;
-        if (regime_out) regime_out[b] = linear ? 1 : 0;
+        // algo 2: the exact closed form's regime; algo 0/1: whether the closed-form
+        // comparator was taken (onepass)
+        if (regime_out) regime_out[b] = (exact ? linear : closed) ? 1 : 0;
     }
 }
 
@@ -440,9 +472,10 @@ namespace {
 template <int C, int P, bool CH>
 hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int algo,
                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                         double* xl, double* cmp_out, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), OCX_SHAPE(L->G), 0, st, zt, yt, L->B, L->T, L->d, L->G, algo, eta0, cmp,
-                       reg, cum, comp, xl, cmp_out, regime);
+                         double* xl, double* cmp_out, int* regime, int onepass, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), OCX_SHAPE(L->G), 0, st, zt, yt,
+                       L->B, L->T, L->d, L->G, algo, eta0, cmp, reg, cum, comp, xl, cmp_out,
+                       regime, onepass);
     return hipGetLastError();
 }
 
@@ -479,10 +512,10 @@ bool ocx_supported_C(int C) {
 
 hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                          double* xl, hipStream_t st, double* cmp_out, int* regime) {
+                          double* xl, hipStream_t st, double* cmp_out, int* regime, int onepass) {
     if (L->G == 0) return hipSuccess;
     OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
-                 st)
+                 onepass, st)
 }
 
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,

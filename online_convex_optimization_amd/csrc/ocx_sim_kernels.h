@@ -6,11 +6,13 @@
 #include "../../include/ocx.h"
 
 bool ocx_supported_C(int C);
-// algo: 0 FTRL, 1 FTL, 2 exact FTL (l2 ball, linear regime; see ocx_sim.hip)
+// algo: 0 FTRL, 1 FTL, 2 exact FTL (l2 ball, linear regime; see ocx_sim.hip).
+// onepass: rows are known to satisfy ||z_t|| <= 1 (g(T) sampler): the comparator loss of
+// FTL(theta_T) in closed form where the kernel can certify it (ocx_alg_kernel)
 hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
                           double* xl, hipStream_t st, double* cmp_out = nullptr,
-                          int* regime = nullptr);
+                          int* regime = nullptr, int onepass = 0);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);
@@ -36,9 +38,11 @@ hipError_t ocx_launch_gen_seek(uint64_t base_seed, int64_t T_seed, int64_t run0,
 hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const uint64_t* st_in,
                                    uint64_t* st_out, const uint64_t* lab_in, uint64_t* lab_out,
                                    double* zt, double* ytl, hipStream_t st);
+// mode 0 pass A, 1 pass B, 2 closed-form comparator (ocx_stream.hip); unclean [B + 1]
 hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                 int64_t t0, int alg_flag, double eta0, int mode, double* theta,
-                                double* cum, double* comp, double* regret, hipStream_t st);
+                                double* cum, double* comp, double* regret, hipStream_t st,
+                                double* unclean = nullptr);
 // FTRL and exact FTL in one pass (ocx_ftrl_exact.hip)
 hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,

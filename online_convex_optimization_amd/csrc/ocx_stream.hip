@@ -13,15 +13,21 @@
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
-// mode 0: loop steps [t0, t0+Tc) of fast_algorithms.py:99-111, theta/cum in & out.
+// mode 0: loop steps [t0, t0+Tc) of fast_algorithms.py:99-111, theta/cum in & out;
+//         unclean[b] (nullable) is set to 1 when a step's sub-gradient is not −y_t/2.
 // mode 1: comparator loss of those steps with x* = FTL(theta_state); when regret_out
-//         is non-null (last chunk) also regret = cum - comp.
+//         is non-null (last chunk) also regret = cum - comp (only where unclean[b] != 0
+//         when unclean is given: the clean sequences took the closed form in mode 2).
+// mode 2: no rows read; for every sequence with unclean[b] == 0 the closed-form
+//         comparator loss (ocx_alg_kernel, onepass) t0/2 − ||theta_T|| (t0 = T here)
+//         and regret; unclean[B] (one past the sequences) = 1 when any sequence needs
+//         the second pass.
 template <int C, int P, bool CHAIN, int NB>
 __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t Tc,
     int64_t G, int64_t t0, int alg_flag, double eta0, int mode, double* __restrict__ theta_state,
     int64_t Dp, double* __restrict__ cum_state, double* __restrict__ comp_state,
-    double* __restrict__ regret_out) {
+    double* __restrict__ regret_out, double* __restrict__ unclean) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -41,6 +47,23 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
 #pragma unroll
     for (int j = 0; j < C; ++j) th[j] = live ? th_row[j] : 0.0;
 
+    if (mode == 2) {
+        double p[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+        const double nrm = sqrt(ocx_total<C, P, CHAIN>(p, lane));
+        if (live && c == 0) {
+            if (unclean[b] == 0.0) {
+                const double comp = 0.5 * (double)t0 - nrm;
+                comp_state[b] = comp;
+                regret_out[b] = cum_state[b] - comp;
+            } else {
+                unclean[B] = 1.0;  // plain store of the same value by every writer
+            }
+        }
+        return;
+    }
+
     ocx_d2 zb[NB][K];
     double yb[NB];
 #pragma unroll
@@ -52,6 +75,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
 
     if (mode == 0) {
         const bool ftl = (alg_flag != 0);
+        bool clean = true;
         double cum = live ? cum_state[b] : 0.0;
         OcxScaleTable sct;  // FTRL scales, 64 steps at a time (long chains)
         for (int64_t u0 = 0; u0 < Tc; u0 += NB) {
@@ -81,6 +105,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                     const double diff = q - yb[u];
                     cum += 0.5 * fabs(diff);
                     const double gq = ocx_grad(diff);
+                    clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
 #pragma unroll
                     for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);
                 }
@@ -90,6 +115,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
 #pragma unroll
             for (int j = 0; j < C; ++j) th_row[j] = th[j];
             if (c == 0) cum_state[b] = cum;
+            if (c == 0 && unclean != nullptr && !clean) unclean[b] = 1.0;
         }
     } else {
         double xs[C];
@@ -121,7 +147,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
         }
         if (live && c == 0) {
             comp_state[b] = comp;
-            if (regret_out) regret_out[b] = cum_state[b] - comp;
+            if (regret_out && (unclean == nullptr || unclean[b] != 0.0))
+                regret_out[b] = cum_state[b] - comp;
         }
     }
 }
@@ -130,18 +157,20 @@ namespace {
 template <int C, int P, bool CH>
 hipError_t launch_chunk_cp(const ocx_layout* L, const double* zt, const double* yt, int64_t t0,
                            int alg_flag, double eta0, int mode, double* th, double* cum,
-                           double* comp, double* reg, hipStream_t st) {
+                           double* comp, double* reg, double* unclean, hipStream_t st) {
     hipLaunchKernelGGL((ocx_alg_chunk_kernel<C, P, CH, nb_for(C, P)>),
-                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode,
-                       th, L->Dp, cum, comp, reg);
+                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0,
+                       st, zt, yt, L->B, L->T, L->G, t0, alg_flag, eta0, mode, th, L->Dp, cum,
+                       comp, reg, unclean);
     return hipGetLastError();
 }
 }  // namespace
 
 hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                 int64_t t0, int alg_flag, double eta0, int mode, double* theta,
-                                double* cum, double* comp, double* regret, hipStream_t st) {
-    if (L->G == 0 || L->T == 0) return hipSuccess;
+                                double* cum, double* comp, double* regret, hipStream_t st,
+                                double* unclean) {
+    if (L->G == 0 || (L->T == 0 && mode != 2)) return hipSuccess;
     OCX_DISPATCH(launch_chunk_cp, L, zt, yt, t0, alg_flag, eta0, mode, theta, cum, comp, regret,
-                 st)
+                 unclean, st)
 }

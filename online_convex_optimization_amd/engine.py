@@ -219,32 +219,23 @@ def max_regret(regrets: np.ndarray) -> float:
 def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
              eta0: float = SQRT2, devices: Optional[Sequence[int]] = None,
              lanes_per_seq: int = LANES_BEST) -> dict:
-    """empirical_worst_case_thresholds on one or several GPUs of this process.
+    """empirical_worst_case_thresholds on one or several GPUs of this process
+    (``ocx_gT_sweep_devices``).
 
-    Runs are split into contiguous shards, one per device, each generated and
-    simulated on its own GPU (threads: ctypes releases the GIL); the per-shard
-    regrets are concatenated in run order.  Returns {T: (g(T), regrets[runs])}."""
-    devs = list(devices) if devices else [0]
-    out = {}
-    for T in T_grid:
-        T = int(T)
-        bounds = np.linspace(0, runs, len(devs) + 1).astype(np.int64)
-        parts = [None] * len(devs)
-
-        def work(i):
-            lo, hi = int(bounds[i]), int(bounds[i + 1])
-            parts[i] = gT_regrets(T, hi - lo, base_seed=base_seed, d=d, eta0=eta0, run0=lo,
-                                  lanes_per_seq=lanes_per_seq, device=devs[i])
-
-        if len(devs) == 1:
-            work(0)
-        else:
-            import concurrent.futures as cf
-            with cf.ThreadPoolExecutor(len(devs)) as ex:
-                list(ex.map(work, range(len(devs))))
-        regs = np.concatenate(parts)
-        out[T] = (max_regret(regs), regs)
-    return out
+    For every T the runs are split into contiguous shards, one per device, each generated
+    and simulated on its own GPU by a native host thread; the per-shard regrets land in
+    run order.  Returns {T: (g(T), regrets[runs])}."""
+    devs = [int(v) for v in devices] if devices else [0]
+    grid = np.ascontiguousarray([int(T) for T in T_grid], dtype=np.int64)
+    regs = np.zeros((len(grid), int(runs)), dtype=np.float64)
+    gmax = np.zeros(len(grid), dtype=np.float64)
+    dv = (ctypes.c_int * len(devs))(*devs)
+    if base_seed < 0 or base_seed >= 2 ** 64:
+        raise ValueError("base_seed must be in [0, 2**64)")
+    _lib.call("ocx_gT_sweep_devices", grid.ctypes.data_as(_lib.c_i64p), len(grid), int(runs),
+              int(base_seed), int(d), float(eta0), dv, len(devs), int(lanes_per_seq),
+              ptr(gmax), ptr(regs))
+    return {int(T): (float(gmax[i]), regs[i]) for i, T in enumerate(grid)}
 
 
 # ---------------------------------------------------------------------------
@@ -263,6 +254,9 @@ class DeviceBatch:
         import torch
         self.torch = torch
         self.L = _lib.layout(B, T, d, lanes_per_seq)
+        # bit-exact modes keep the reference's two-pass comparator sum (see simulate_alg)
+        self.exact = lanes_per_seq == LANES_EXACT or lanes_per_seq < 0
+        self.rows_clipped = False  # set by generate_gT: every ||z_t|| <= 1
         self.device = torch.device("cuda", device)
         with torch.cuda.device(self.device):
             self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -300,6 +294,7 @@ class DeviceBatch:
         """Fill z/y with _rng(base_seed, T, run0 + b) sequences (on device)."""
         _lib.call("ocx_dev_gen_gT", self._lp(), int(base_seed), int(run0), self.z.data_ptr(),
                   self.y.data_ptr(), self._sp)
+        self.rows_clipped = True
         return self
 
     FAMILIES = {"iid": 1, "massart": 2, "flip": 3, "switching": 4}
@@ -319,6 +314,7 @@ class DeviceBatch:
                                      ).to(self.device)
             if rs.numel() != self.L.B or si.numel() != self.L.B:
                 raise ValueError("need one run seed and one stream id per sequence")
+        self.rows_clipped = False
         _lib.call("ocx_dev_gen_family", self._lp(), fam,
                   rs.data_ptr() if rs is not None else None,
                   si.data_ptr() if si is not None else None, float(p), int(block_len),
@@ -338,19 +334,33 @@ class DeviceBatch:
                                  ).to(self.device, torch.float64).contiguous()
         if tuple(zt.shape) != (self.L.B, self.L.T, self.L.d) or tuple(yt.shape) != (self.L.B, self.L.T):
             raise ValueError("z/y shape does not match the batch")
+        self.rows_clipped = False
         _lib.call("ocx_dev_pack", self._lp(), zt.data_ptr(), yt.data_ptr(), self.z.data_ptr(),
                   self.y.data_ptr(), self._sp)
         self._keep = self._hold(zt, yt)
         return self
 
     def simulate_alg(self, alg_flag: int = 0, eta0: float = SQRT2, comparator=None,
-                     x_last=None):
-        """Launch the FTRL/FTL kernel; results land in self.regret/cum/comp (async)."""
+                     x_last=None, closed_comparator: Optional[bool] = None, closed_out=None):
+        """Launch the FTRL/FTL kernel; results land in self.regret/cum/comp (async).
+
+        ``closed_comparator`` (default: the batch holds g(T)-sampler rows, which are
+        clipped to ||z_t|| <= 1, and its layout is not a bit-exact mode) takes the
+        comparator loss in closed form, T/2 - ||theta_T||, wherever the kernel can certify
+        it, and so reads z once instead of twice (ocx_dev_simulate_alg_ex,
+        OCX_ALG_CLIPPED_ROWS); the regret then equals the reference's up to rounding.
+        Passing True for packed data asserts that its rows satisfy ||z_t|| <= 1.
+        ``closed_out`` ([B] int32 device tensor, optional) receives 1 per sequence that took
+        the closed form, 0 where the kernel streamed the second pass."""
         cp = comparator.data_ptr() if comparator is not None else None
         xp = x_last.data_ptr() if x_last is not None else None
-        _lib.call("ocx_dev_simulate_alg", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        if closed_comparator is None:
+            closed_comparator = self.rows_clipped and not self.exact and comparator is None
+        flags = _lib.OCX_ALG_CLIPPED_ROWS if closed_comparator else 0
+        _lib.call("ocx_dev_simulate_alg_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   int(alg_flag), float(eta0), cp, self.regret.data_ptr(), self.cum.data_ptr(),
-                  self.comp.data_ptr(), xp, self._sp)
+                  self.comp.data_ptr(), xp, flags,
+                  closed_out.data_ptr() if closed_out is not None else None, self._sp)
         return self.regret
 
     def simulate_smart(self, thresh, eta0: float = SQRT2, switch_step=None):

@@ -33,6 +33,17 @@ def close(a, b, tol=TOL):
     return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
 
 
+def close_closed(a, b, T):
+    """Bar for the closed-form comparator (T/2 - ||theta_T||, OCX_ALG_CLIPPED_ROWS) against
+    the reference's sequential sum of T terms: that sum's own rounding error grows like
+    eps*T^1.5 (measured 3.3e-11 absolute, 7e-13 relative to the regret, at T = 1e4), so
+    |diff| <= max(1e-12 * max(1, |ref|), 4 eps T^1.5).  North star: 1e-6 relative."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    tol = np.maximum(TOL * np.maximum(1.0, np.abs(b)), 4 * 2.22e-16 * float(T) ** 1.5)
+    return np.all(np.abs(a - b) <= tol)
+
+
 # ------------------------------------------------------------------ golden vectors
 def test_simulate_alg_golden_bitexact(ocx, golden):
     fa = ocx["fa"]
@@ -242,11 +253,13 @@ def test_full_size_properties(ocx):
     r1 = exact.simulate_alg().clone()
     r2 = exact.simulate_alg().clone()
     auto = eng.DeviceBatch(B, T, d, lanes_per_seq=0).generate_gT(base_seed=0, run0=0)
-    ra = auto.simulate_alg().clone()
+    ra = auto.simulate_alg().clone()  # butterfly sums + closed-form comparator
+    ra2 = auto.simulate_alg(closed_comparator=False).clone()
     torch.cuda.synchronize()
     assert torch.equal(r1, r2)
     assert auto.L.P > 1
-    assert torch.all((ra - r1).abs() <= TOL * torch.clamp(r1.abs(), min=1.0))
+    assert torch.all((ra2 - r1).abs() <= TOL * torch.clamp(r1.abs(), min=1.0))
+    assert close_closed(ra.cpu().numpy(), r1.cpu().numpy(), T)
     r1 = r1.cpu().numpy()
     for b in (0, 1, 777, B - 1):
         zr, yr = O.gT_sample(0, T, b, d)
@@ -341,15 +354,16 @@ def test_best_mode_default(ocx, T, d, runs, exact):
     eng, lib = ocx["engine"], ocx["lib"]
     L = lib.layout(runs, T, d, eng.LANES_BEST)
     assert bool(L.P == 1 or L.chain) == exact
-    reg = eng.gT_regrets(T, runs, base_seed=9, d=d)
+    reg = eng.gT_regrets(T, runs, base_seed=9, d=d)  # + the closed-form comparator
     assert np.array_equal(reg, eng.gT_regrets(T, runs, base_seed=9, d=d,
                                               lanes_per_seq=eng.LANES_BEST))
+    ex = eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=1)
     for r in (0, runs // 3, runs - 1):
         z, y = O.gT_sample(9, T, r, d)
         ref = O.simulate_alg(z, y, 0, SQ2)
-        assert reg[r] == ref if exact else close(reg[r], ref), (r, reg[r], ref)
-    if exact:
-        assert np.array_equal(reg, eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=1))
+        assert close_closed(reg[r], ref, T), (r, reg[r], ref)
+        assert ex[r] == ref
+    assert close_closed(reg, ex, T)
 
 
 @pytest.mark.parametrize("P", [1, 0])
@@ -476,3 +490,92 @@ def test_release_buffers_then_regrow(ocx):
     eng.release_buffers()  # idempotent
     b = eng.gT_regrets(300, 40, d=64, lanes_per_seq=1)
     assert np.array_equal(a, b)
+
+
+# ------------------------------------------------------------------ closed-form comparator
+@pytest.mark.parametrize("B,T,d,P", [(700, 300, 64, 128), (9000, 60, 64, 128), (300, 500, 5, 0),
+                                     (40, 200, 1024, 128), (130, 1000, 16, 4), (64, 1, 3, 0)])
+def test_closed_comparator_matches_two_pass(ocx, B, T, d, P):
+    """OCX_ALG_CLIPPED_ROWS on g(T)-sampler rows: the loop is untouched (cum_loss bit for
+    bit), the comparator loss T/2 - ||theta_T|| agrees with the streamed sum within the
+    sum's own rounding, and so do the regrets (also against the oracle)."""
+    import torch
+    eng = ocx["engine"]
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).generate_gT(base_seed=5, run0=3)
+    assert db.rows_clipped and not db.exact
+    r_two = db.simulate_alg(closed_comparator=False).clone()
+    cum_two, comp_two = db.cum.clone(), db.comp.clone()
+    flag = torch.zeros(B, dtype=torch.int32, device=db.device)
+    r_one = db.simulate_alg(closed_out=flag).clone()
+    torch.cuda.synchronize()
+    assert bool(torch.all(flag == 1))  # the sampler's sequences are all clean
+    assert torch.equal(db.cum, cum_two)
+    assert close_closed(db.comp.cpu().numpy(), comp_two.cpu().numpy(), T)
+    assert close_closed(r_one.cpu().numpy(), r_two.cpu().numpy(), T)
+    r_one = r_one.cpu().numpy()
+    for b in (0, B // 2, B - 1):
+        z, y = O.gT_sample(5, T, 3 + b, d)
+        assert close_closed(r_one[b], O.simulate_alg(z, y, 0, SQ2), T), b
+    # FTL (alg_flag 1) takes the same closed form
+    f_two = db.simulate_alg(1, closed_comparator=False).clone()
+    f_one = db.simulate_alg(1).clone()
+    torch.cuda.synchronize()
+    assert close_closed(f_one.cpu().numpy(), f_two.cpu().numpy(), T)
+
+
+@pytest.mark.parametrize("P", [-1, 128, 0])
+def test_closed_comparator_falls_back(ocx, P):
+    """Sequences whose sub-gradients are not all -y_t/2 (a label of 0.5, a zero row with a
+    zero label: an exact tie) take the second pass, bit-identical to the two-pass kernel;
+    the clean sequences of the same waves keep the closed form."""
+    import torch
+    eng = ocx["engine"]
+    rng = np.random.default_rng(3)
+    B, T, d = 70, 120, 8
+    z = rng.standard_normal((B, T, d))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    y[5, 17] = 0.5                       # not ±1
+    z[9, 0] = 0.0
+    y[9, 0] = 0.0                        # q - y == 0: the sub-gradient is 0, not -y/2
+    y[40, T - 1] = 0.25
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y)
+    assert not db.rows_clipped
+    two = db.simulate_alg(closed_comparator=False).clone()
+    flag = torch.full((B,), 7, dtype=torch.int32, device=db.device)
+    one = db.simulate_alg(closed_comparator=True, closed_out=flag).clone()
+    torch.cuda.synchronize()
+    two, one, flag = two.cpu().numpy(), one.cpu().numpy(), flag.cpu().numpy()
+    assert set(np.nonzero(flag == 0)[0]) == {5, 9, 40} and np.all(flag[flag != 0] == 1)
+    for b in (5, 9, 40):
+        assert one[b] == two[b], b
+    assert close_closed(one, two, T)
+    for b in (0, 5, 9, 40, B - 1):
+        assert close_closed(one[b], O.simulate_alg(z[b], y[b], 0, SQ2), T), b
+
+
+def test_gT_sweep_c_entry(ocx):
+    """ocx_gT_sweep (the C-level multi-device sweep, ngpus=1 here) and its device-list form
+    against per-T gT_regrets calls."""
+    import ctypes
+    eng, lib = ocx["engine"], ocx["lib"]
+    grid = np.array([30, 200, 1000], dtype=np.int64)
+    runs = 50
+    gmax = np.zeros(3)
+    regs = np.zeros((3, runs))
+    lib.call("ocx_gT_sweep", grid.ctypes.data_as(lib.c_i64p), 3, runs, 7, 16, SQ2, 1,
+             lib.ptr(gmax), lib.ptr(regs))
+    gmax2 = np.zeros(3)
+    lib.call("ocx_gT_sweep", grid.ctypes.data_as(lib.c_i64p), 3, runs, 7, 16, SQ2, 0,
+             lib.ptr(gmax2), None)
+    assert np.array_equal(gmax, gmax2)
+    for i, T in enumerate(grid):
+        ref = eng.gT_regrets(int(T), runs, base_seed=7, d=16)
+        assert np.array_equal(regs[i], ref)
+        assert gmax[i] == eng.max_regret(ref)
+    with pytest.raises(ValueError):
+        lib.call("ocx_gT_sweep", grid.ctypes.data_as(lib.c_i64p), 3, runs, 7, 16, SQ2, 999,
+                 lib.ptr(gmax), None)
+    out = eng.gT_sweep(list(grid), runs, base_seed=7, d=16, devices=[0, 0, 0])
+    for i, T in enumerate(grid):
+        assert np.array_equal(out[int(T)][1], regs[i]) and out[int(T)][0] == gmax[i]

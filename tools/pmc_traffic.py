@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--T", type=int, required=True)
     ap.add_argument("--d", type=int, required=True)
     ap.add_argument("--P", type=int, required=True)
+    ap.add_argument("--passes", type=int, default=2,
+                    help="passes over z per launch: 2 = streamed comparator, 1 = closed form")
     ap.add_argument("--out", default="profiles/traffic.json")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
@@ -59,8 +61,9 @@ def main():
     w_kib = sum(write) / len(write)
     read_bytes = 2.0 * f_kib * 1024.0
     write_bytes = w_kib * 1024.0
-    alg = a.B * a.T * 2 * (8 * a.d + 8)
+    alg = a.B * a.T * a.passes * (8 * a.d + 8)
     out = {"kernel": a.kernel, "B": a.B, "T": a.T, "d": a.d, "P": a.P,
+           "comparator": "closed" if a.passes == 1 else "two-pass",
            "dispatches": len(fetch), "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,
            "hbm_read_bytes_per_launch": read_bytes, "hbm_write_bytes_per_launch": write_bytes,
            "hbm_bytes_per_launch": read_bytes + write_bytes,
