@@ -231,6 +231,18 @@ int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const doub
                           double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                           double* comp_ftl, double* cmp_action, int32_t* regime, void* stream);
 
+/* ocx_dev_ftrl_vs_exact with options.  flags OCX_ALG_CLOSED_COMPARATOR (or
+ * OCX_ALG_CLIPPED_ROWS): for every sequence whose rows the kernel finds inside the unit
+ * ball (||z_t||^2 <= 1 + 1e-12, summed in the step anyway) with labels +-1, both comparator
+ * losses take their closed form T/2 + x.theta_e/2 (every loss is linear on the ball and
+ * theta_e = -S_T is in registers), so such waves read z once instead of twice; the rest
+ * stream the second pass.  Equal to the sequential sums up to their rounding. */
+#define OCX_ALG_CLOSED_COMPARATOR 2
+int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                             double* comp_ftl, double* cmp_action, int32_t* regime, int flags,
+                             void* stream);
+
 /* fast_algorithms.py:118-164 on device; thresh [B] device. */
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                            const double* thresh, double eta0, double* regret,

@@ -78,11 +78,14 @@ SIGNATURES = {
     "ocx_dev_max_regret": (c_int, [c_vp, c_i64, c_vp, c_vp]),
     "ocx_dev_simulate_alg_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "ocx_dev_ftrl_vs_exact_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "ocx_gT_sweep": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double, c_int, c_dp, c_dp]),
     "ocx_gT_sweep_devices": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double,
                                      ctypes.POINTER(c_int), c_int, c_int, c_dp, c_dp]),
 }
 OCX_ALG_CLIPPED_ROWS = 1
+OCX_ALG_CLOSED_COMPARATOR = 2
 
 _lib = None
 _lock = threading.Lock()

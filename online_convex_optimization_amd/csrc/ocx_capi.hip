@@ -328,6 +328,22 @@ int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const doub
     return OCX_OK;
 }
 
+int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
+                             double* comp_ftl, double* cmp_action, int32_t* regime, int flags,
+                             void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (L->B && (!cum_ftrl || !cum_exact || !comp_exact || !regime))
+        return fail(OCX_E_INVALID, "NULL output buffer");
+    if (flags & ~(OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR))
+        return fail(OCX_E_INVALID, "unknown flags");
+    OCX_HIP(ocx_launch_ftrl_exact(L, z_tiled, y_tiled, eta0, cum_ftrl, cum_exact, comp_exact,
+                                  comp_ftl, cmp_action, regime, (hipStream_t)stream,
+                                  flags ? 1 : 0));
+    return OCX_OK;
+}
+
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                            const double* thresh, double eta0, double* regret,
                            int64_t* switch_step, void* stream) {
@@ -533,8 +549,12 @@ int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t
                             cx->yt.as<double>(), st));
     double* o = cx->out.as<double>();
     int* rg = reinterpret_cast<int*>(o + B * (4 + d));
+    // outside the bit-exact modes the comparator losses take their closed form where the
+    // kernel certifies the regime (ocx_dev_ftrl_vs_exact_ex)
+    const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
     OCX_HIP(ocx_launch_ftrl_exact(&L, cx->zt.as<double>(), cx->yt.as<double>(), eta0, o, o + B,
-                                  o + 2 * B, o + 3 * B, o + 4 * B, rg, st));
+                                  o + 2 * B, comp_ftl ? o + 3 * B : nullptr, o + 4 * B, rg, st,
+                                  onepass));
     std::vector<double> h((size_t)B * (4 + d));
     OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));

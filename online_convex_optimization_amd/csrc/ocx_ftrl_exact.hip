@@ -9,7 +9,11 @@
 //           closed form of ocx_sim.hip's algo 2, with its regime check) per step;
 //   pass 2  the loss of x* = FTL(θ_e) = S_T/‖S_T‖, and optionally of FTL(θ_r) (the
 //           comparator fast_algorithms.simulate_alg itself would use).
-// Two HBM passes instead of four.  Per step the FTRL sums (‖sθ_r‖², z·sθ_r) and the
+// Two HBM passes instead of four.  With `onepass`, a sequence whose rows all have
+// ‖z_t‖² <= 1 + 1e-12 (checked here: the ‖z‖² sum is part of the step) and labels ±1 needs
+// no pass 2: on the unit ball every loss is linear, ½|z·x − y| = ½(1 − y z·x), so the loss
+// of any comparator x is T/2 − ½ x·S_T = T/2 + ½ x·θ_e, and θ_e = −S_T is in registers.
+// A wave streams pass 2 only for sequences outside that regime.  Per step the FTRL sums (‖sθ_r‖², z·sθ_r) and the
 // exact-FTL sums (‖θ_e‖², ‖z‖²) run as one 4-way chain; then z·x_e.
 #include "ocx_device_math.h"
 #include "ocx_dispatch.h"
@@ -70,7 +74,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t d, int64_t G, double eta0, double* __restrict__ cum_r, double* __restrict__ cum_e,
     double* __restrict__ comp_e, double* __restrict__ comp_f, double* __restrict__ cmp_out,
-    int* __restrict__ regime_out) {
+    int* __restrict__ regime_out, int onepass) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
 #pragma unroll
     for (int j = 0; j < C; ++j) tr[j] = te[j] = 0.0;
     bool linear = true;
+    bool clipped = true;  // every ‖z_t‖² <= 1 + 1e-12 (closed-form comparators)
 
     ocx_d2 zb[NB][K];
     double yb[NB];
@@ -141,6 +146,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
                 cr += 0.5 * fabs(dr);
                 ce += 0.5 * fabs(qe - yv);
                 linear = linear && tot[3] <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+                clipped = clipped && tot[3] <= 1.0 + 1e-12;
                 const double gr = ocx_grad(dr);
 #pragma unroll
                 for (int j = 0; j < C; ++j) {
@@ -155,7 +161,12 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
     // ---- pass 2: comparator x* = FTL(θ_e); optionally FTL(θ_r) ----
     double xs[C], xf[C];
     ocx_action_ftl<C, P, CHAIN>(te, xs, lane);
-    if (comp_f != nullptr) ocx_action_ftl<C, P, CHAIN>(tr, xf, lane);
+    if (comp_f != nullptr) {
+        ocx_action_ftl<C, P, CHAIN>(tr, xf, lane);
+    } else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) xf[j] = 0.0;
+    }
     if (cmp_out != nullptr && b < B) {
 #pragma unroll
         for (int j = 0; j < C; ++j) {
@@ -163,14 +174,16 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
             if (jj < d) cmp_out[b * d + jj] = xs[j];
         }
     }
+    const bool closed = onepass && ((linear && clipped) || b >= B);
+    const bool pass2 = __ballot(!closed) != 0;  // wave-uniform
+    double ke = 0.0, kf = 0.0;
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u)
-        if (u < T) {
+        if (u < T && pass2) {
             ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
             yb[u] = yp[u * S];
         }
-    double ke = 0.0, kf = 0.0;
-    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+    for (int64_t t0 = 0; t0 < (pass2 ? T : 0); t0 += NB) {
 #pragma unroll
         for (int u = 0; u < NB; ++u) {
             const int64_t t = t0 + u;
@@ -194,6 +207,15 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
             }
         }
     }
+    if (__ballot(closed) != 0) {  // wave-uniform: the sums cross lanes
+        double q2[2];
+        ocx_totals<C, P, CHAIN, 2>(
+            [&](int j, int k) -> double { return te[j] * (k ? xf[j] : xs[j]); }, q2, lane);
+        if (closed) {
+            ke = 0.5 * (double)T + 0.5 * q2[0];
+            kf = 0.5 * (double)T + 0.5 * q2[1];
+        }
+    }
     if (c == 0 && b < B) {
         cum_r[b] = cr;
         cum_e[b] = ce;
@@ -207,17 +229,20 @@ namespace {
 template <int C, int P, bool CH>
 hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt, double eta0,
                         double* cum_r, double* cum_e, double* comp_e, double* comp_f,
-                        double* cmp_out, int* regime, hipStream_t st) {
+                        double* cmp_out, int* regime, int onepass, hipStream_t st) {
     hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C, P, false)>),
-                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e,
-                       comp_e, comp_f, cmp_out, regime);
+                       ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0,
+                       st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e, comp_e, comp_f,
+                       cmp_out, regime, onepass);
     return hipGetLastError();
 }
 }  // namespace
 
 hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,
-                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st) {
+                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st,
+                                 int onepass) {
     if (L->G == 0) return hipSuccess;
-    OCX_DISPATCH(launch_fe_cp, L, zt, yt, eta0, cum_r, cum_e, comp_e, comp_f, cmp_out, regime, st)
+    OCX_DISPATCH(launch_fe_cp, L, zt, yt, eta0, cum_r, cum_e, comp_e, comp_f, cmp_out, regime,
+                 onepass, st)
 }

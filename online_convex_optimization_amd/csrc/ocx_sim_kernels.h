@@ -46,4 +46,5 @@ hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const dou
 // FTRL and exact FTL in one pass (ocx_ftrl_exact.hip)
 hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,
-                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st);
+                                 double* comp_f, double* cmp_out, int* regime, hipStream_t st,
+                                 int onepass = 0);

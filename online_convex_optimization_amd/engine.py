@@ -388,11 +388,14 @@ class DeviceBatch:
                   regime.data_ptr(), self._sp)
         return regime
 
-    def ftrl_vs_exact(self, eta0: float = SQRT2, comp_ftl=None, cmp_action=None, regime=None):
+    def ftrl_vs_exact(self, eta0: float = SQRT2, comp_ftl=None, cmp_action=None, regime=None,
+                      closed_comparator: Optional[bool] = None):
         """ftrl_vs_exact_batch on the resident batch: self.cum gets FTRL's cumulative loss,
         self.comp the exact comparator's loss, self.cum_exact exact FTL's (allocated on first
         use); ``comp_ftl`` [B] (device, optional) the loss of FTL(theta_ftrl).  Returns the
-        regime flags."""
+        regime flags.  ``closed_comparator`` (default: not a bit-exact layout) takes both
+        comparator losses in closed form for the sequences the kernel finds in the unit-ball
+        regime (ocx_dev_ftrl_vs_exact_ex): one HBM pass instead of two."""
         torch = self.torch
         n = max(self.L.B, 1)
         with self._on_stream():
@@ -400,11 +403,13 @@ class DeviceBatch:
                 self.cum_exact = torch.zeros(n, dtype=torch.float64, device=self.device)
             if regime is None:
                 regime = torch.zeros(n, dtype=torch.int32, device=self.device)
-        _lib.call("ocx_dev_ftrl_vs_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        if closed_comparator is None:
+            closed_comparator = not self.exact
+        _lib.call("ocx_dev_ftrl_vs_exact_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
                   cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
-                  self._sp)
+                  _lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0, self._sp)
         return regime
 
     def max_regret(self, out=None):

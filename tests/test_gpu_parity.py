@@ -455,8 +455,8 @@ def test_ftrl_vs_exact_fused_matches_oracle(ocx, B, T, d):
             want = [rc, rp, fr[1], fr[0], ff[2]]
             if P != 4:
                 assert got == want and np.array_equal(r["action"][b], ra), (P, b)
-            else:
-                assert close(got, want) and close(r["action"][b], ra), (P, b)
+            else:  # butterfly sums + closed-form comparator losses
+                assert close_closed(got, want, T) and close(r["action"][b], ra), (P, b)
     if B and T:
         with pytest.raises(NotImplementedError):
             eng.ftrl_vs_exact_batch(2.0 * z, y, SQ2)
@@ -579,3 +579,39 @@ def test_gT_sweep_c_entry(ocx):
     out = eng.gT_sweep(list(grid), runs, base_seed=7, d=16, devices=[0, 0, 0])
     for i, T in enumerate(grid):
         assert np.array_equal(out[int(T)][1], regs[i]) and out[int(T)][0] == gmax[i]
+
+
+@pytest.mark.parametrize("P", [128, 0])
+def test_ftrl_vs_exact_closed_form(ocx, P):
+    """DeviceBatch.ftrl_vs_exact: closed-form comparator losses (OCX_ALG_CLOSED_COMPARATOR)
+    vs the two-pass kernel on sampler rows (all in the regime: one pass), and on packed rows
+    with a few sequences outside it (those stream pass 2, bit-identical to two-pass)."""
+    import torch
+    eng = ocx["engine"]
+    B, T, d = 600, 400, 64
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).generate_gT(base_seed=8)
+    cf2 = torch.zeros(B, dtype=torch.float64, device=db.device)
+    cf1 = torch.zeros_like(cf2)
+    db.ftrl_vs_exact(SQ2, comp_ftl=cf2, closed_comparator=False)
+    two = [t.clone() for t in (db.cum, db.cum_exact, db.comp)]
+    db.ftrl_vs_exact(SQ2, comp_ftl=cf1)
+    one = [db.cum, db.cum_exact, db.comp]
+    torch.cuda.synchronize()
+    assert torch.equal(one[0], two[0]) and torch.equal(one[1], two[1])
+    assert close_closed(one[2].cpu().numpy(), two[2].cpu().numpy(), T)
+    assert close_closed(cf1.cpu().numpy(), cf2.cpu().numpy(), T)
+    # rows outside the ball in a few sequences: those take the second pass
+    rng = np.random.default_rng(2)
+    z = rng.standard_normal((70, 120, 8))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((70, 120)) < 0.5, -1.0, 1.0)
+    z[3, 10] *= 1.5
+    z[50, 0] *= (1.0 + 1e-9) / np.linalg.norm(z[50, 0])  # just outside the ball
+    pk = eng.DeviceBatch(70, 120, 8, lanes_per_seq=P).pack(z, y)
+    pk.ftrl_vs_exact(SQ2, closed_comparator=False)
+    a = pk.comp.clone()
+    pk.ftrl_vs_exact(SQ2)
+    torch.cuda.synchronize()
+    a, bb = a.cpu().numpy(), pk.comp.cpu().numpy()
+    assert a[3] == bb[3] and a[50] == bb[50]
+    assert close_closed(bb, a, 120)

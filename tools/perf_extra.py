@@ -96,17 +96,18 @@ def config3(args):
     engine.release_buffers()  # the sweeps' cached HBM, if run in the same process
     db = engine.DeviceBatch(Bb, T, d, lanes_per_seq=1)
     results = {}
-    for variant in ("fused", "separate", "fused"):
+    for variant in ("fused", "separate", "fused", "fused_best"):
+        lanes = 128 if variant == "fused_best" else 1  # best: closed-form comparators
         sync()
         t0 = time.perf_counter()
         out = []
         for r0 in range(0, trials, Bb):
             B = min(Bb, trials - r0)
-            if B != db.L.B:
+            if B != db.L.B or lanes != (1 if db.exact else 128):
                 del db
-                db = engine.DeviceBatch(B, T, d, lanes_per_seq=1)
+                db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes)
             db.generate_gT(0, r0)
-            if variant == "fused":
+            if variant.startswith("fused"):
                 cf = torch.zeros(B, dtype=torch.float64, device=db.device)
                 regime = db.ftrl_vs_exact(math.sqrt(2), comp_ftl=cf)
                 exact = db.cum - db.comp
@@ -130,8 +131,10 @@ def config3(args):
                           "mean_regret_exact_minus_fast": float(dd.mean()),
                           "max_abs_diff": float(np.abs(dd).max()),
                           "mean_regret_ftl_exact": float(res[2].mean())}), flush=True)
+    rb, rf = results["fused_best"], results["fused"]
     print(json.dumps({"what": "config3_fused_equals_separate",
-                      "bitexact": bool(np.array_equal(results["fused"], results["separate"]))}),
+                      "bitexact": bool(np.array_equal(results["fused"], results["separate"])),
+                      "best_vs_exact_max_rel": float((np.abs(rb - rf) / np.maximum(1.0, np.abs(rf))).max())}),
           flush=True)
 
 
