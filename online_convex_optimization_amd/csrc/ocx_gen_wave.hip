@@ -378,7 +378,10 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 // squares uses all 64 lanes (8 leaves of 128, 8 accumulators each: the leaf and tree
 // order of NumPy's recursion is the 64-lane butterfly) and every store instruction
 // writes whole contiguous plane segments; DF = 0: any d.
-template <int MODE, int DF>
+// LR (DF = 64 only): the low-LDS form for few-stream batches: 7 rows per epilogue batch
+// (7·64 + 63 pending normals fit 512 doubles) so the ring is 4 KB per wave and six waves
+// per SIMD fit the LDS; the default form's 8-row batches need 1024 (4 waves per SIMD).
+template <int MODE, int DF, bool LR = false>
 __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
     const int lg2P = __builtin_ctz((unsigned)(2 * P));
     // rows leave the ring in batches of R: the sums of squares of a batch run side by
     // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
-    const int R = batch_rows(d);
+    const int R = LR ? 7 : batch_rows(d);
     // store map for Dp <= 64: lane → (row of the pass, coordinate j), RP rows per pass
     const int RP = Dp <= 64 ? 64 / Dp : 1;
     const int jl = Dp <= 64 ? lane % Dp : lane;
@@ -526,7 +529,18 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
                     sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
                 }
                 const int sc_stride = d < 8 ? 1 : 8;
-                if (DF == 64) {
+                if (DF == 64 && LR) {
+                    // 7-row batches in a 512 ring: rows of 64 never wrap, but a batch
+                    // does, so each row gets its own masked base
+                    double* zp = zt + zoff + t * 128;
+                    for (int r = 0; r < nrows; ++r) {
+                        const double scr = __hiloint2double(
+                            __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
+                            __builtin_amdgcn_readlane(__double2loint(sc), r * sc_stride));
+                        const unsigned ro = (tailp + 64u * (unsigned)r) & (unsigned)rmask;
+                        OCX_GEN_STORE(ring[ro + (unsigned)lane] * scr, zp + r * 128);
+                    }
+                } else if (DF == 64) {
                     // whole rows of 64, never wrapping (see leaf_sumsq): lane j stores
                     // coordinate j of each row, at immediate LDS offsets from one base
                     const double* rp = ring + (tailp & (unsigned)rmask) + lane;
@@ -623,20 +637,21 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
 
 namespace {
 
-int ring_doubles(int64_t d, int DF) {
+int ring_doubles(int64_t d, int DF, bool LR = false) {
     if (DF == 1024) return 1024;  // exactly one row: rounds stop at the row's end
+    if (LR) return 512;           // 7 rows + one round's normals (ocx_gen_wave_kernel, LR)
     // a full batch of rows plus one round of normals
     int rb = 128;
     while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
     return rb;
 }
 
-template <int MODE, int DF>
+template <int MODE, int DF, bool LR = false>
 hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
                           int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
                           double* ytl, const uint64_t* st_in, uint64_t* st_out,
                           const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
-    const int rb = (MODE == 0) ? ring_doubles(d, DF) : 0;
+    const int rb = (MODE == 0) ? ring_doubles(d, DF, LR) : 0;
     const size_t lds =
         (MODE == 0) ? (size_t)(rb + (d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
     // resident waves: fill the GPU once, sequences spread evenly over the waves
@@ -650,7 +665,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
         const int n = std::atoi(ev);
         if (n > 0 && n < cus) cus = n;
     }
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF, LR>,
                                                      kWaveBlock, lds);
     if (e != hipSuccess) return e;
     int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
@@ -664,7 +679,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
     const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));
-    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF>), dim3(blocks), dim3(kWaveBlock), lds, st,
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR>), dim3(blocks), dim3(kWaveBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
                        st_out, lab_in, lab_out, rb, nwaves);
     return hipGetLastError();
@@ -677,9 +692,23 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
                        uint64_t* lab_out, hipStream_t st) {
     // the kernel counts a sequence's normals in 32 bits
     if ((MODE == 0 ? T : T_seed) * d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
-    if (d == 64 && (MODE == 1 || (int64_t)P * C == 64))
+    if (d == 64 && (MODE == 1 || (int64_t)P * C == 64)) {
+        // Few streams (the capacity-limited T = 1e5 batch): the default form's 4 waves per
+        // SIMD would give each wave two or more whole sequences while half the wave slots
+        // stay empty; the low-LDS form's 6 waves per SIMD give every stream its own wave
+        // (d = 64, T = 1e5, 4900 streams: 161 -> 117 ms).  Beyond that the default form is
+        // faster (32768 x 1e4: 77.9 vs 82.7 ms at 6 waves; profiles/r02_gen_ring640_probe.jsonl).
+        int dev = 0, cus = 256;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        if (MODE == 0 && nseq > (int64_t)cus * 16 && nseq <= (int64_t)cus * 24)
+            return launch_wave_df<MODE, 64, true>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G,
+                                                  zt, ytl, st_in, st_out, lab_in, lab_out, st);
         return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
                                         st_in, st_out, lab_in, lab_out, st);
+    }
     if (MODE == 0 && d == 1024 && (int64_t)P * C == 1024 && P <= 64)
         return launch_wave_df<MODE, 1024>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt,
                                           ytl, st_in, st_out, lab_in, lab_out, st);
