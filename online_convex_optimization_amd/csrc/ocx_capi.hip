@@ -152,7 +152,7 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     // T = 1e5, 3328 sequences measured 69 ms at 16 x 4 (62 % of 8 TB/s) against 75 ms at
     // 8 x 8, 82 ms at 32 x 2 and 104 ms for the exact 8-lane chain; d = 1024: 52 ms
     // (81 %) against 102 ms exact (profiles/r02_fewwave_block_shapes.jsonl)
-    bool best_tree = false;
+    bool best_tree = false;  // OCX_LANES_BEST fell back to butterfly sums
     if (lanes_per_seq == OCX_LANES_BEST) {
         ocx_layout Le;
         if (int rc = ocx_layout_init(B, T, d, 1, &Le)) return rc;
@@ -171,9 +171,20 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     int64_t p_min = 1;
     while (p_min < 64 && ceil_div(d, p_min) > 16) p_min *= 2;
     int64_t p_max = 1;
-    const int64_t c_min = best_tree ? 4 : 2;  // fewest coordinates per lane
+    const int64_t c_min = 2;  // fewest coordinates per lane
     while (p_max < 64 && ceil_div(d, p_max * 2) >= c_min) p_max *= 2;
-    if (lanes_per_seq == 0) {
+    if (best_tree) {
+        // OCX_LANES_BEST where exact chains would be latency-bound: butterfly lanes of 8
+        // coordinates up to d = 128 from 4096 sequences on (their 8-step register ring;
+        // d = 64, T = 1e5, 4900 sequences, one pass over z: 52 ms at 8 x 8 vs 59 at 16 x 4
+        // and 71 at 4 x 16), 4 below (3328: 46 ms at 16 x 4 vs 52 at 8 x 8: twice the
+        // waves), 32 from d = 512 (d = 1024, 3400 sequences: 44 ms at 32 x 32 vs 46 at
+        // 64 x 16), 16 between (profiles/r02_fewwave_lanes_onepass.jsonl, r02_best2_probe.jsonl)
+        const int64_t ct = d >= 512 ? 32 : (d <= 128 ? (B >= 4096 ? 8 : 4) : 16);
+        int64_t p = 1;
+        while (p < 64 && ceil_div(d, p) > ct) p *= 2;
+        P = (int)p;
+    } else if (lanes_per_seq == 0) {
         // auto: enough lanes for ~8 wavefronts per CU (131072 lanes on
         // 256 CUs) when B allows.
         int64_t p_lanes = 1;
@@ -663,7 +674,10 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
             const int64_t wmax = (int64_t)cus * 4;
             ocx_layout Lc;
             if (int rc = ocx_layout_init(chunk, T, d, lanes_per_seq, &Lc)) return rc;
-            if (Lc.G > wmax && Lc.G < 2 * wmax && Lc.C >= 16) {
+            // (two-pass only: with the closed-form comparator the generator's throughput,
+            // which grows with the streams per batch, dominates: d = 1024, T = 1e4
+            // measured 1.68e8 timesteps/s at 3400 per batch vs 1.50e8 at 2048)
+            if (!onepass && Lc.G > wmax && Lc.G < 2 * wmax && Lc.C >= 16) {
                 chunk = wmax * Lc.S;
                 nbat = (R + chunk - 1) / chunk;
                 chunk = (R + nbat - 1) / nbat;

@@ -78,7 +78,8 @@ def test_auto_layout_choices():
 
 def test_best_layout_choices():
     """OCX_LANES_BEST (128): the exact layout while its chains stay under 8 lanes, else
-    butterfly sums with at least 4 coordinates per lane."""
+    butterfly sums with 8 coordinates per lane up to d = 128 (4 below 4096 sequences), 32
+    from d = 512."""
     best = 128
     L = _lib.layout(32768, 10, 64, best)       # the bench batch: exact, 4-lane chain
     assert (L.P, L.C, L.chain) == (4, 16, 1)
@@ -86,12 +87,14 @@ def test_best_layout_choices():
     assert (L.P, L.chain) == (1, 0)
     L = _lib.layout(768, 10, 5, best)          # the drivers' batches: exact
     assert (L.P, L.C, L.chain) == (4, 2, 1)
-    L = _lib.layout(4900, 10, 64, best)        # few-wave (T = 1e5 batch): butterfly 16 x 4
+    L = _lib.layout(4900, 10, 64, best)        # few-wave (T = 1e5 batch): butterfly 8 x 8
+    assert (L.P, L.C, L.chain) == (8, 8, 0)
+    L = _lib.layout(3328, 10, 64, best)        # fewer: twice the waves, 16 x 4
     assert (L.P, L.C, L.chain) == (16, 4, 0)
-    L = _lib.layout(3328, 10, 64, best)
-    assert (L.P, L.C, L.chain) == (16, 4, 0)
-    L = _lib.layout(2048, 10, 1024, best)      # configs[4]: butterfly 64 x 16
-    assert (L.P, L.C, L.chain) == (64, 16, 0)
+    L = _lib.layout(2048, 10, 1024, best)      # configs[4]: butterfly 32 x 32
+    assert (L.P, L.C, L.chain) == (32, 32, 0)
+    L = _lib.layout(500, 10, 200, best)        # between: 16 coordinates per lane
+    assert (L.P, L.C, L.chain) == (16, 16, 0)
     L = _lib.layout(1, 10, 3, best)            # a single short sequence: exact
     assert L.P * L.C >= 3 and (L.P == 1 or L.chain == 1)
 
