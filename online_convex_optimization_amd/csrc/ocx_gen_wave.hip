@@ -122,8 +122,69 @@ struct WaveStream {
     ocx_u128 Ak, Dk;
 };
 
+// ---- (a * b + d) mod 2^128 with a, d per lane and b wave-uniform (SGPRs) --------------
+// Ten 32x32 partial products: six v_mad_u64_u32 (the 64-bit columns, each keeping its
+// carry-out in an SGPR pair instead of re-deriving it), four v_mul_lo_u32 for the top
+// column, and the carries folded in with v_addc: 18 VALU instructions where the
+// compiler's __int128 lowering spends 25 (it zero-extends every 32-bit carry into a
+// VGPR pair with v_mov).  Operand order keeps one scalar source per VOP3.
+__device__ __forceinline__ uint64_t mad64c(uint32_t a, uint32_t b, uint64_t c, uint64_t& cy) {
+    uint64_t r;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=&v"(r), "=s"(cy) : "v"(a), "s"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint64_t mad64z(uint32_t a, uint32_t b) {
+    uint64_t r, cy;
+    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=&v"(r), "=s"(cy) : "v"(a), "s"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t add32c(uint32_t a, uint32_t b, uint64_t& cy) {
+    uint32_t r;
+    asm volatile("v_add_co_u32_e64 %0, %1, %2, %3" : "=v"(r), "=s"(cy) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t addc32(uint32_t a, uint32_t b, uint64_t cin, uint64_t& cy) {
+    uint32_t r;
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(a), "v"(b), "s"(cin));
+    return r;
+}
+__device__ __forceinline__ uint32_t addc32z(uint32_t a, uint64_t cin) {
+    uint32_t r;
+    uint64_t cy;
+    asm volatile("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(cy) : "v"(a), "s"(cin));
+    return r;
+}
+__device__ __forceinline__ ocx_u128 mul_add_u128(ocx_u128 a, ocx_u128 b, ocx_u128 d) {
+#ifdef OCX_GEN_INT128_MUL  // reference form (tuning A/B)
+    return a * b + d;
+#else
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), a2 = (uint32_t)(a >> 64),
+                   a3 = (uint32_t)(a >> 96);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32), b2 = (uint32_t)(b >> 64),
+                   b3 = (uint32_t)(b >> 96);
+    uint64_t ca, cb, cc, c1, c3, cx;
+    const uint64_t T = mad64c(a0, b0, (uint64_t)d, ca);               // a0b0 + d_lo
+    const uint64_t M = mad64c(a1, b0, mad64z(a0, b1), cb);            // a0b1 + a1b0 (cb: 2^96)
+    const uint32_t l1 = add32c((uint32_t)(T >> 32), (uint32_t)M, cc);  // bits 32..63
+    uint64_t H = mad64c(a0, b2, (uint64_t)(d >> 64), cx);             // bits 64..127, mod 2^64
+    H = mad64c(a1, b1, H, cx);
+    H = mad64c(a2, b0, H, cx);
+    const uint32_t X = a0 * b3 + a1 * b2 + a2 * b1 + a3 * b0;          // bits 96..127
+    uint32_t hl = addc32((uint32_t)H, (uint32_t)(M >> 32), cc, c1);
+    hl = addc32(hl, 0u, ca, c3);
+    uint32_t hh = addc32((uint32_t)(H >> 32), X, c1, cx);
+    hh = addc32z(hh, c3);
+    hh = addc32z(hh, cb);
+    const uint64_t lo = ((uint64_t)l1 << 32) | (uint32_t)T;
+    const uint64_t hi = ((uint64_t)hh << 32) | hl;
+    return ((ocx_u128)hi << 64) | lo;
+#endif
+}
+
 __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u128 Gk) {
-    w.base = g.state;
+    // every lane holds the same state; reading it from lane 0 makes it provably uniform,
+    // so the round loop keeps the base in SGPRs (the multiply's scalar operand)
+    w.base = rl128(g.state, 0);
     w.inc = g.inc;
     w.Dk = g.inc * Gk;
 }
@@ -134,13 +195,15 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 template <bool RING>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
-    const ocx_u128 s = w.Ak * w.base + w.Dk;
+    const ocx_u128 s = mul_add_u128(w.Ak, w.base, w.Dk);
     const uint64_t r = xsl_rr(s);
     const int idx = (int)(r & 0xff);
     const uint64_t r8 = r >> 8;
     const uint64_t rabs = (r8 >> 1) & kMask52;
     double x = u52_to_double(rabs) * tb.wi[idx];
-    if (r8 & 1) x = -x;
+    // sign bit 8 of the draw → the sign of x (x = -x, -0.0 included), one xor
+    x = __hiloint2double(__double2hiint(x) ^ (int)(((uint32_t)r & 0x100u) << 23),
+                         __double2loint(x));
 #ifdef OCX_GEN_TUNE_NO_PARSE  // tuning only: every draw accepted (wrong normals)
     const bool fast = true;
 #else
@@ -221,7 +284,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         const TailOut o = zig_tail((uint64_t)st, (uint64_t)(st >> 64), (uint64_t)w.inc,
                                    (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
         if (RING && lane == 0) ring[(head + n) & rmask] = o.v;
-        w.base = ((ocx_u128)o.hi << 64) | o.lo;
+        w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
         return n + 1;
     }
     w.base = rl128(s, m - 1);
@@ -344,10 +407,12 @@ constexpr int kWaveBlock = 256;
 // Waves per SIMD the register allocation must allow.  For the d = 64 kernel 6 waves
 // (80 VGPRs, a few cold spills) measured 6 % faster than the unconstrained 104 VGPRs
 // (4 waves); its LDS (6 KB tables + 4 x 4 KB rings per block) also admits 6.
+// The default d = 64 form's 8 KB ring holds the LDS to four waves per SIMD, so it gets the
+// four-wave register budget (no spills); the few-stream form (LR, 4 KB ring) runs six.
 #ifndef OCX_GENW_MIN_WAVES
-#define OCX_GENW_MIN_WAVES_FOR(DF) ((DF) == 64 ? 6 : ((DF) == 1024 ? 4 : 1))
+#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? 4 : 1))
 #else
-#define OCX_GENW_MIN_WAVES_FOR(DF) OCX_GENW_MIN_WAVES
+#define OCX_GENW_MIN_WAVES_FOR(DF, LR) OCX_GENW_MIN_WAVES
 #endif
 
 // rows per batch leaving the ring (see the kernel)
@@ -382,7 +447,7 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 // (7·64 + 63 pending normals fit 512 doubles) so the ring is 4 KB per wave and six waves
 // per SIMD fit the LDS; the default form's 8-row batches need 1024 (4 waves per SIMD).
 template <int MODE, int DF, bool LR = false>
-__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_gen_wave_kernel(
+__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
@@ -606,7 +671,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
         if (lab_in != nullptr) {
             ocx_u128 ls, li;
             load_state6(lab_in + 6 * b, ls, li, buf32, has32);
-            w.base = ls;
+            w.base = rl128(ls, 0);
         }
         int64_t tl = 0;
         if (has32 && T > 0) {
@@ -617,7 +682,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF)) void ocx_ge
         while (tl < T) {
             const int64_t left = T - tl;
             const int ndraw = left >= 128 ? 64 : (int)((left + 1) / 2);
-            const ocx_u128 st = w.Ak * w.base + w.Dk;
+            const ocx_u128 st = mul_add_u128(w.Ak, w.base, w.Dk);
             const uint64_t r = xsl_rr(st);
             const int64_t t0 = tl + 2 * lane;
             if (lane < ndraw) {
