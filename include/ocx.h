@@ -106,18 +106,24 @@ int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_
                              int64_t* switch_step, int lanes_per_seq, int device);
 
 /* exact_ftl.py:423-453 run_ftl_exact (compute_prefix_actions :280-303 + replay
- * :306-333) for the l2 ball (norm must be 0), batched, in the closed form that is exact
- * when every ||z_t|| <= 1 and y_t = ±1: the prefix minimiser of ½Σ|z_i·x − y_i| over the
- * ball is S_t/||S_t|| (0 if S_t = 0), S_t = Σ_{i<t} y_i z_i.  regime [B] (int32, 1 = the
- * data were in that regime, within 1e-6 on ||z_t||²); outside it the returned numbers
- * are not the SOCP solution and callers must reject them.  cmp_action [B][d] nullable
- * = actions[T] (the exact comparator of the whole sequence).  The reference solves an
- * SOCP with cvxpy, absent here: parity unpinned. */
+ * :306-333) over the unit ball of `norm` (0 l2, 1 l1, 2 linf; ExactFTLNoClip :83-105),
+ * batched, in the closed form that is exact when every row's dual norm is <= 1 and
+ * y_t = ±1 (then |z_i·x| <= 1 on the ball and ½Σ|z_i·x − y_i| = ½(t − x·S_t),
+ * S_t = Σ_{i<t} y_i z_i): the prefix minimiser maximises x·S_t over the ball:
+ *   l2   S_t/||S_t|| (0 if S_t = 0)            regime ||z_t||_2^2 <= 1 + 1e-6
+ *   l1   sign(S_j*) e_j*, j* = first argmax |S_j|  regime max_j |z_tj| <= 1 + 1e-12
+ *   linf sign(S_t) componentwise (0 where S_tj = 0)  regime sum_j |z_tj| <= 1 + 1e-12
+ * regime [B] (int32, 1 = the data were in that regime); outside it the returned numbers
+ * are not the SOCP/LP solution and callers must reject them.  Where the maximiser is not
+ * unique (S_t = 0, ties in |S_j|, zero coordinates under linf) the solver's choice is
+ * arbitrary; the engine returns the point above.  cmp_action [B][d] nullable = actions[T]
+ * (the exact comparator of the whole sequence).  The reference solves an SOCP / LP with
+ * cvxpy, absent here: parity unpinned, validated against scipy's solvers. */
 int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                         int norm, double* cum_loss, double* comp_loss, double* cmp_action,
                         int32_t* regime, int lanes_per_seq, int device);
 
-/* exact_ftl.py:280-303 compute_prefix_actions (ExactFTLNoClip, norm 0 = l2), batched:
+/* exact_ftl.py:280-303 compute_prefix_actions (ExactFTLNoClip, `norm` as above), batched:
  * actions [B][T+1][d] row-major, actions[b][t] = the exact FTL solution of prefix length
  * t, in the closed form of ocx_ftl_exact_batch (S_t/||S_t||, 0 for S_t = 0), with the
  * same regime flags (int32 [B], required).  Replaying these actions (ocx_replay_batch)
@@ -127,7 +133,7 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
                                  int lanes_per_seq, int device);
 
 /* exact_ftl_driver.py:157-186 per sequence, batched, in one read of the data: exact FTL
- * (as ocx_ftl_exact_batch, l2 closed form) and FTRL (fast_algorithms.py:88-111 order,
+ * (as ocx_ftl_exact_batch over the `norm` ball) and FTRL (fast_algorithms.py:88-111 order,
  * eta0) against the exact comparator actions[T] (exact_ftl.py:399-420 run_ftrl with
  * comparator_action).  Outputs [B]: cum_ftrl, cum_exact, comp_exact (the loss of
  * actions[T], shared by both regrets: FTRL = cum_ftrl - comp_exact, exact FTL =
@@ -136,7 +142,7 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
  * (int32, required; see ocx_ftl_exact_batch). */
 int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                            double* comp_ftl, double* cmp_action, int32_t* regime,
+                            double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
                             int lanes_per_seq, int device);
 
 /* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
@@ -215,7 +221,7 @@ int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const do
                             double* cum_loss, double* comp_loss, double* x_last, int flags,
                             int32_t* closed_out, void* stream);
 
-/* ocx_ftl_exact_batch on device (norm 0 = l2 only). */
+/* ocx_ftl_exact_batch on device (`norm` 0 l2, 1 l1, 2 linf). */
 int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
                       double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
                       void* stream);
@@ -231,17 +237,18 @@ int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const doub
                           double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                           double* comp_ftl, double* cmp_action, int32_t* regime, void* stream);
 
-/* ocx_dev_ftrl_vs_exact with options.  flags OCX_ALG_CLOSED_COMPARATOR (or
- * OCX_ALG_CLIPPED_ROWS): for every sequence whose rows the kernel finds inside the unit
- * ball (||z_t||^2 <= 1 + 1e-12, summed in the step anyway) with labels +-1, both comparator
+/* ocx_dev_ftrl_vs_exact with options: `norm` of the exact side (0 l2, 1 l1, 2 linf, as
+ * ocx_ftl_exact_batch), and flags OCX_ALG_CLOSED_COMPARATOR (or OCX_ALG_CLIPPED_ROWS):
+ * for l2 and every sequence whose rows the kernel finds inside the unit ball
+ * (||z_t||^2 <= 1 + 1e-12, summed in the step anyway) with labels +-1, both comparator
  * losses take their closed form T/2 + x.theta_e/2 (every loss is linear on the ball and
  * theta_e = -S_T is in registers), so such waves read z once instead of twice; the rest
  * stream the second pass.  Equal to the sequential sums up to their rounding. */
 #define OCX_ALG_CLOSED_COMPARATOR 2
 int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                              double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                             double* comp_ftl, double* cmp_action, int32_t* regime, int flags,
-                             void* stream);
+                             double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
+                             int flags, void* stream);
 
 /* fast_algorithms.py:118-164 on device; thresh [B] device. */
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,

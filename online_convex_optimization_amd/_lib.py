@@ -60,7 +60,7 @@ SIGNATURES = {
                                            c_vp]),
     "ocx_ftrl_vs_exact_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_double, c_dp, c_dp,
                                         c_dp, c_dp, c_dp, ctypes.POINTER(ctypes.c_int32), c_int,
-                                        c_int]),
+                                        c_int, c_int]),
     "ocx_dev_ftrl_vs_exact": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_replay_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_dp, c_int]),
@@ -79,7 +79,7 @@ SIGNATURES = {
     "ocx_dev_simulate_alg_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "ocx_dev_ftrl_vs_exact_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
-                                         c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+                                         c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "ocx_gT_sweep": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double, c_int, c_dp, c_dp]),
     "ocx_gT_sweep_devices": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double,
                                      ctypes.POINTER(c_int), c_int, c_int, c_dp, c_dp]),

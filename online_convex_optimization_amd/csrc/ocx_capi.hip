@@ -306,11 +306,11 @@ int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* 
                       double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
                       void* stream) {
     if (int rc = check_layout(L)) return rc;
-    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (L->B && !regime) return fail(OCX_E_INVALID, "regime output is required");
     OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, 2, 0.0, nullptr, nullptr, cum_loss, comp_loss,
-                           nullptr, (hipStream_t)stream, cmp_action, regime));
+                           nullptr, (hipStream_t)stream, cmp_action, regime, 0, norm));
     return OCX_OK;
 }
 
@@ -318,12 +318,12 @@ int ocx_dev_ftl_prefix_actions(const ocx_layout* L, const double* z_tiled,
                                const double* y_tiled, int norm, double* actions,
                                int32_t* regime, void* stream) {
     if (int rc = check_layout(L)) return rc;
-    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (L->B && (!regime || (L->d > 0 && !actions)))
         return fail(OCX_E_INVALID, "NULL output buffer");
-    OCX_HIP(ocx_launch_prefix_actions(L, z_tiled, y_tiled, actions, regime,
-                                      (hipStream_t)stream));
+    OCX_HIP(ocx_launch_prefix_actions(L, z_tiled, y_tiled, actions, regime, (hipStream_t)stream,
+                                      norm));
     return OCX_OK;
 }
 
@@ -341,8 +341,9 @@ int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const doub
 
 int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                              double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                             double* comp_ftl, double* cmp_action, int32_t* regime, int flags,
-                             void* stream) {
+                             double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
+                             int flags, void* stream) {
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (L->B && (!cum_ftrl || !cum_exact || !comp_exact || !regime))
@@ -351,7 +352,7 @@ int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const d
         return fail(OCX_E_INVALID, "unknown flags");
     OCX_HIP(ocx_launch_ftrl_exact(L, z_tiled, y_tiled, eta0, cum_ftrl, cum_exact, comp_exact,
                                   comp_ftl, cmp_action, regime, (hipStream_t)stream,
-                                  flags ? 1 : 0));
+                                  flags ? 1 : 0, norm));
     return OCX_OK;
 }
 
@@ -471,7 +472,7 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
                         int32_t* regime, int lanes_per_seq, int device) {
     ocx_layout L;
     if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
-    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (B == 0) return OCX_OK;
     if ((T * d > 0 && !z) || (T > 0 && !y) || !regime) return fail(OCX_E_INVALID, "NULL argument");
     DevCtx* cx;
@@ -491,7 +492,7 @@ int ocx_ftl_exact_batch(const double* z, const double* y, int64_t B, int64_t T, 
     double* o = cx->out.as<double>();
     int* rg = reinterpret_cast<int*>(o + B * (2 + d));
     OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 2, 0.0, nullptr, nullptr,
-                           o, o + B, nullptr, st, o + 2 * B, rg));
+                           o, o + B, nullptr, st, o + 2 * B, rg, 0, norm));
     std::vector<double> h((size_t)B * (2 + d));
     OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));
@@ -507,7 +508,7 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
                                  int lanes_per_seq, int device) {
     ocx_layout L;
     if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
-    if (norm != 0) return fail(OCX_E_UNSUPPORTED, "exact FTL: only the l2 ball (norm 0)");
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (B == 0) return OCX_OK;
     if ((T * d > 0 && !z) || (T > 0 && !y) || !regime || (d > 0 && !actions))
         return fail(OCX_E_INVALID, "NULL argument");
@@ -528,7 +529,7 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
                             cx->yt.as<double>(), st));
     int* rg = cx->out.as<int>();
     OCX_HIP(ocx_launch_prefix_actions(&L, cx->zt.as<double>(), cx->yt.as<double>(),
-                                      cx->araw.as<double>(), rg, st));
+                                      cx->araw.as<double>(), rg, st, norm));
     if (na) OCX_HIP(hipMemcpyAsync(actions, cx->araw.p, na * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipStreamSynchronize(st));
@@ -537,10 +538,11 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
 
 int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                            double* comp_ftl, double* cmp_action, int32_t* regime,
+                            double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
                             int lanes_per_seq, int device) {
     ocx_layout L;
     if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (B == 0) return OCX_OK;
     if ((T * d > 0 && !z) || (T > 0 && !y) || !cum_ftrl || !cum_exact || !comp_exact || !regime)
         return fail(OCX_E_INVALID, "NULL argument");
@@ -565,7 +567,7 @@ int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t
     const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
     OCX_HIP(ocx_launch_ftrl_exact(&L, cx->zt.as<double>(), cx->yt.as<double>(), eta0, o, o + B,
                                   o + 2 * B, comp_ftl ? o + 3 * B : nullptr, o + 4 * B, rg, st,
-                                  onepass));
+                                  onepass, norm));
     std::vector<double> h((size_t)B * (4 + d));
     OCX_HIP(hipMemcpyAsync(h.data(), o, h.size() * 8, hipMemcpyDeviceToHost, st));
     OCX_HIP(hipMemcpyAsync(regime, rg, (size_t)B * 4, hipMemcpyDeviceToHost, st));

@@ -274,6 +274,54 @@ __device__ __forceinline__ void ocx_action_ftl(const double (&th)[C], double (&x
     for (int j = 0; j < C; ++j) x[j] = (nsq == 0.0) ? 0.0 : sc * th[j];
 }
 
+// ---------------------------------------------------------------------------
+// Exact FTL over the l1 and linf unit balls (exact_ftl.py:83-105 norm='l1' / 'linf') in
+// the closed form of their linear regime (see ocx_sim.hip, algo 2): with theta = −S_t
+// the prefix minimiser maximises x·S_t over the ball:
+//   l1   x = sign(S_j*) e_j*, j* = the first coordinate of largest |S_j| (0 if S = 0);
+//   linf x_j = sign(S_j) (0 where S_j = 0).
+// Ties (several j*, or S_j = 0 under linf) leave the SOCP/LP solution non-unique; the
+// engine's choice is the one above.  norm codes: 0 l2, 1 l1, 2 linf.
+// ---------------------------------------------------------------------------
+template <int C, int P>
+__device__ __forceinline__ void ocx_action_exact_poly(const double (&th)[C], double (&x)[C],
+                                                      int norm, int lane) {
+    if (norm == 2) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) x[j] = th[j] > 0.0 ? -1.0 : (th[j] < 0.0 ? 1.0 : 0.0);
+        return;
+    }
+    const int c = lane % P;
+    double best = -1.0;
+    int bj = 0;
+#pragma unroll
+    for (int j = 0; j < C; ++j) {
+        const double v = fabs(th[j]);
+        if (v > best) {  // strict: the first of equal values
+            best = v;
+            bj = c * C + j;
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < P; m <<= 1) {  // (value, index) max over the P lanes, lowest index
+        const double ob = __shfl_xor(best, m, 64);
+        const int oj = __shfl_xor(bj, m, 64);
+        if (ob > best || (ob == best && oj < bj)) {
+            best = ob;
+            bj = oj;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j)
+        x[j] = (best > 0.0 && c * C + j == bj) ? (th[j] > 0.0 ? -1.0 : 1.0) : 0.0;
+}
+
+// Is row z inside the regime of the `norm` ball's closed form: its dual norm <= 1
+// (l2: ||z||_2^2 <= 1 + 1e-6, the bar of round 1; l1 ball: max_j |z_j| <= 1 + 1e-12;
+// linf ball: sum_j |z_j| <= 1 + 1e-12)?  Every lane of the sequence gets the answer.
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ bool ocx_dual_ok(const ocx_d2* z, int norm, int lane);
+
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
     double p[C];
@@ -440,3 +488,20 @@ __device__ __forceinline__ double ocx_comp_pass2(const ocx_d2* __restrict__ zp,
 }
 
 
+
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ bool ocx_dual_ok(const ocx_d2* z, int norm, int lane) {
+    double p[C];
+    if (norm == 1) {
+        double m = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) m = fmax(m, fabs(ocx_zj(z, j)));
+#pragma unroll
+        for (int k = 1; k < P; k <<= 1) m = fmax(m, __shfl_xor(m, k, 64));
+        return m <= 1.0 + 1e-12;
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) p[j] = norm == 0 ? ocx_zj(z, j) * ocx_zj(z, j) : fabs(ocx_zj(z, j));
+    const double t = ocx_total<C, P, CHAIN>(p, lane);
+    return norm == 0 ? t <= 1.0 + 1e-6 : t <= 1.0 + 1e-12;
+}

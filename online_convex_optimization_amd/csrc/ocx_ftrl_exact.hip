@@ -74,7 +74,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t d, int64_t G, double eta0, double* __restrict__ cum_r, double* __restrict__ cum_e,
     double* __restrict__ comp_e, double* __restrict__ comp_f, double* __restrict__ cmp_out,
-    int* __restrict__ regime_out, int onepass) {
+    int* __restrict__ regime_out, int onepass, int norm) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -136,16 +136,25 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
                     for (int j = 0; j < C; ++j) xr[j] *= f;
                     qr = ocx_zdot<C, P, CHAIN>(z, xr, lane);
                 }
-                // exact FTL: x = FTL(θ_e) (fast_algorithms.py:37-49 form), q = z·x
+                // exact FTL: x = FTL(θ_e) (fast_algorithms.py:37-49 form) for l2, the
+                // l1 / linf closed forms otherwise; q = z·x
                 double xe[C];
-                const double sce = -(1.0 / sqrt(tot[2]));
+                if (norm == 0) {
+                    const double sce = -(1.0 / sqrt(tot[2]));
 #pragma unroll
-                for (int j = 0; j < C; ++j) xe[j] = (tot[2] == 0.0) ? 0.0 : sce * te[j];
+                    for (int j = 0; j < C; ++j) xe[j] = (tot[2] == 0.0) ? 0.0 : sce * te[j];
+                } else {
+                    ocx_action_exact_poly<C, P>(te, xe, norm, lane);
+                }
                 const double qe = ocx_zdot<C, P, CHAIN>(z, xe, lane);
                 const double dr = qr - yv;
                 cr += 0.5 * fabs(dr);
                 ce += 0.5 * fabs(qe - yv);
-                linear = linear && tot[3] <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+                if (norm == 0) {
+                    linear = linear && tot[3] <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+                } else {
+                    linear = linear && ocx_dual_ok<C, P, CHAIN>(z, norm, lane) && fabs(yv) == 1.0;
+                }
                 clipped = clipped && tot[3] <= 1.0 + 1e-12;
                 const double gr = ocx_grad(dr);
 #pragma unroll
@@ -160,7 +169,11 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
 
     // ---- pass 2: comparator x* = FTL(θ_e); optionally FTL(θ_r) ----
     double xs[C], xf[C];
-    ocx_action_ftl<C, P, CHAIN>(te, xs, lane);
+    if (norm == 0) {
+        ocx_action_ftl<C, P, CHAIN>(te, xs, lane);
+    } else {
+        ocx_action_exact_poly<C, P>(te, xs, norm, lane);
+    }
     if (comp_f != nullptr) {
         ocx_action_ftl<C, P, CHAIN>(tr, xf, lane);
     } else {
@@ -174,7 +187,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
             if (jj < d) cmp_out[b * d + jj] = xs[j];
         }
     }
-    const bool closed = onepass && ((linear && clipped) || b >= B);
+    // (l2 only: FTL(θ_r) is a Euclidean unit vector, so its loss needs ‖z_t‖ <= 1)
+    const bool closed = onepass && norm == 0 && ((linear && clipped) || b >= B);
     const bool pass2 = __ballot(!closed) != 0;  // wave-uniform
     double ke = 0.0, kf = 0.0;
 #pragma unroll
@@ -229,11 +243,11 @@ namespace {
 template <int C, int P, bool CH>
 hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt, double eta0,
                         double* cum_r, double* cum_e, double* comp_e, double* comp_f,
-                        double* cmp_out, int* regime, int onepass, hipStream_t st) {
+                        double* cmp_out, int* regime, int onepass, int norm, hipStream_t st) {
     hipLaunchKernelGGL((ocx_ftrl_exact_kernel<C, P, CH, nb_for(C, P, false)>),
                        ocx_grid(L->G, ocx_block_waves(L->G)), dim3(64 * ocx_block_waves(L->G)), 0,
                        st, zt, yt, L->B, L->T, L->d, L->G, eta0, cum_r, cum_e, comp_e, comp_f,
-                       cmp_out, regime, onepass);
+                       cmp_out, regime, onepass, norm);
     return hipGetLastError();
 }
 }  // namespace
@@ -241,8 +255,8 @@ hipError_t launch_fe_cp(const ocx_layout* L, const double* zt, const double* yt,
 hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,
                                  double* comp_f, double* cmp_out, int* regime, hipStream_t st,
-                                 int onepass) {
+                                 int onepass, int norm) {
     if (L->G == 0) return hipSuccess;
     OCX_DISPATCH(launch_fe_cp, L, zt, yt, eta0, cum_r, cum_e, comp_e, comp_f, cmp_out, regime,
-                 onepass, st)
+                 onepass, norm, st)
 }

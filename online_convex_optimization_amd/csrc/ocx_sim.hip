@@ -25,12 +25,14 @@
 // ---------------------------------------------------------------------------
 // fast_algorithms.py:88-115 `_simulate_alg_core` (+ exact_ftl.py:230-277 outputs)
 //   algo 0 FTRL, 1 FTL (the reference's alg_flag 0 / non-zero);
-//   algo 2 exact FTL over the l2 ball (exact_ftl.py:280-333 compute_prefix_actions +
-//          replay) in its linear regime: when every ||z_t|| <= 1 and y_t = ±1,
-//          ½Σ|z_i·x − y_i| = ½(t − x·S_t) on the ball, so the prefix minimiser is
-//          S_t/||S_t|| (0 if S_t = 0) with S_t = Σ_{i<t} y_i z_i — the FTL action of
-//          theta = −S_t.  regime_out[b] reports whether the data were in that regime
-//          (max ||z_t||² <= 1 + 1e-6 and |y_t| == 1); the caller rejects otherwise.
+//   algo 2 exact FTL over the unit ball of `norm` (0 l2, 1 l1, 2 linf; exact_ftl.py:83-105,
+//          :280-333 compute_prefix_actions + replay) in its linear regime: when every row's
+//          dual norm is <= 1 and y_t = ±1, |z_i·x| <= 1 on the ball and
+//          ½Σ|z_i·x − y_i| = ½(t − x·S_t), so the prefix minimiser maximises x·S_t,
+//          S_t = Σ_{i<t} y_i z_i: S_t/||S_t|| for l2 (0 if S_t = 0; the FTL action of
+//          theta = −S_t), ocx_action_exact_poly for l1 / linf.  regime_out[b] reports
+//          whether the data were in that regime (ocx_dual_ok and |y_t| == 1); the caller
+//          rejects otherwise.
 // cmp_out [B][d] (nullable) receives the comparator action of the second pass.
 // ---------------------------------------------------------------------------
 // Waves per SIMD the register allocation of the FTRL kernel must allow (tuning knob:
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     int64_t d, int64_t G, int algo, double eta0, const double* __restrict__ comparator,
     double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
     double* __restrict__ x_last, double* __restrict__ cmp_out, int* __restrict__ regime_out,
-    int onepass) {
+    int onepass, int norm) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -103,7 +105,11 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                         q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t + 1, eta0, x, lane);
                     }
                 } else {
-                    ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                    if (exact && norm != 0) {
+                        ocx_action_exact_poly<C, P>(th, x, norm, lane);
+                    } else {
+                        ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+                    }
                     q = ocx_zdot<C, P, CHAIN>(zb[u], x, lane);
                 }
                 if (x_last != nullptr && t == T - 1 && b < B) {
@@ -118,11 +124,8 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 double gq = ocx_grad(diff);
                 clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
                 if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
-                    double p[C];
-#pragma unroll
-                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * ocx_zj(zb[u], j);
-                    const double zz = ocx_total<C, P, CHAIN>(p, lane);
-                    linear = linear && zz <= 1.0 + 1e-6 && fabs(yb[u]) == 1.0;
+                    linear = linear && ocx_dual_ok<C, P, CHAIN>(zb[u], norm, lane) &&
+                             fabs(yb[u]) == 1.0;
                     gq = -yb[u];
                 }
 #pragma unroll
@@ -155,6 +158,8 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
             const int64_t jj = (int64_t)c * C + j;
             xs[j] = (b < B && jj < d) ? comparator[b * d + jj] : 0.0;
         }
+    } else if (exact && norm != 0) {
+        ocx_action_exact_poly<C, P>(th, xs, norm, lane);
     } else {
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
     }
@@ -366,7 +371,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_replay_kernel(
 template <int C, int P, bool CHAIN>
 __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
-    int64_t d, int64_t G, double* __restrict__ actions, int* __restrict__ regime_out) {
+    int64_t d, int64_t G, double* __restrict__ actions, int* __restrict__ regime_out, int norm) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -388,7 +393,11 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
     bool linear = true;
     for (int64_t t = 0; t <= T; ++t) {
         double x[C];
-        ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+        if (norm != 0) {
+            ocx_action_exact_poly<C, P>(th, x, norm, lane);
+        } else {
+            ocx_action_ftl<C, P, CHAIN>(th, x, lane);
+        }
         if (b < B) {
 #pragma unroll
             for (int j = 0; j < C; ++j)
@@ -398,11 +407,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
         ocx_d2 z[K];
         ocx_load_tile<C>(z, zp + t * tstride, kst);
         const double yv = yp[t * S];
-        double p[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) p[j] = ocx_zj(z, j) * ocx_zj(z, j);
-        const double zz = ocx_total<C, P, CHAIN>(p, lane);
-        linear = linear && zz <= 1.0 + 1e-6 && fabs(yv) == 1.0;
+        linear = linear && ocx_dual_ok<C, P, CHAIN>(z, norm, lane) && fabs(yv) == 1.0;
         const double gq = -yv;
 #pragma unroll
         for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(z, j);
@@ -472,10 +477,11 @@ namespace {
 template <int C, int P, bool CH>
 hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt, int algo,
                          double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                         double* xl, double* cmp_out, int* regime, int onepass, hipStream_t st) {
+                         double* xl, double* cmp_out, int* regime, int onepass, int norm,
+                         hipStream_t st) {
     hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), OCX_SHAPE(L->G), 0, st, zt, yt,
                        L->B, L->T, L->d, L->G, algo, eta0, cmp, reg, cum, comp, xl, cmp_out,
-                       regime, onepass);
+                       regime, onepass, norm);
     return hipGetLastError();
 }
 
@@ -498,8 +504,9 @@ hipError_t launch_replay_cp(const ocx_layout* L, const double* zt, const double*
 
 template <int C, int P, bool CH>
 hipError_t launch_prefix_cp(const ocx_layout* L, const double* zt, const double* yt,
-                            double* actions, int* regime, hipStream_t st) {
-    hipLaunchKernelGGL((ocx_prefix_actions_kernel<C, P, CH>), OCX_SHAPE(L->G), 0, st, zt, yt, L->B, L->T, L->d, L->G, actions, regime);
+                            double* actions, int* regime, int norm, hipStream_t st) {
+    hipLaunchKernelGGL((ocx_prefix_actions_kernel<C, P, CH>), OCX_SHAPE(L->G), 0, st, zt, yt,
+                       L->B, L->T, L->d, L->G, actions, regime, norm);
     return hipGetLastError();
 }
 
@@ -512,10 +519,11 @@ bool ocx_supported_C(int C) {
 
 hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
-                          double* xl, hipStream_t st, double* cmp_out, int* regime, int onepass) {
+                          double* xl, hipStream_t st, double* cmp_out, int* regime, int onepass,
+                          int norm) {
     if (L->G == 0) return hipSuccess;
     OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
-                 onepass, st)
+                 onepass, norm, st)
 }
 
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
@@ -538,9 +546,9 @@ hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double
     OCX_DISPATCH(launch_replay_cp, L, zt, yt, at, cum, comp, st)
 }
 hipError_t ocx_launch_prefix_actions(const ocx_layout* L, const double* zt, const double* yt,
-                                     double* actions, int* regime, hipStream_t st) {
+                                     double* actions, int* regime, hipStream_t st, int norm) {
     if (L->G == 0) return hipSuccess;
-    OCX_DISPATCH(launch_prefix_cp, L, zt, yt, actions, regime, st)
+    OCX_DISPATCH(launch_prefix_cp, L, zt, yt, actions, regime, norm, st)
 }
 
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,

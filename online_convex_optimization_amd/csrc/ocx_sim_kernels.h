@@ -12,7 +12,7 @@ bool ocx_supported_C(int C);
 hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* yt, int algo,
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
                           double* xl, hipStream_t st, double* cmp_out = nullptr,
-                          int* regime = nullptr, int onepass = 0);
+                          int* regime = nullptr, int onepass = 0, int norm = 0);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);
@@ -24,7 +24,7 @@ hipError_t ocx_launch_replay(const ocx_layout* L, const double* zt, const double
                              const double* at, double* cum, double* comp, hipStream_t st);
 // exact FTL prefix actions [B][T+1][d] (closed form, l2 ball; ocx_sim.hip)
 hipError_t ocx_launch_prefix_actions(const ocx_layout* L, const double* zt, const double* yt,
-                                     double* actions, int* regime, hipStream_t st);
+                                     double* actions, int* regime, hipStream_t st, int norm = 0);
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
                            double* ytl, hipStream_t st);
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
@@ -47,4 +47,4 @@ hipError_t ocx_launch_alg_chunk(const ocx_layout* L, const double* zt, const dou
 hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const double* yt,
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,
                                  double* comp_f, double* cmp_out, int* regime, hipStream_t st,
-                                 int onepass = 0);
+                                 int onepass = 0, int norm = 0);

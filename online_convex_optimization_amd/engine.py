@@ -102,28 +102,36 @@ def replay_batch(z, y, actions, *, device: int = 0):
     return cum, comp
 
 
-NORMS = {"l2": 0}
+NORMS = {"l2": 0, "l1": 1, "linf": 2}  # the ball of exact FTL (exact_ftl.py:83-105)
+_DUAL = {"l2": "||z_t||_2 <= 1", "l1": "max_j |z_tj| <= 1", "linf": "sum_j |z_tj| <= 1"}
 
 
-def _reject_out_of_regime(ok: np.ndarray) -> None:
+def _norm_code(norm: str) -> int:
+    if norm not in NORMS:
+        raise ValueError("norm must be one of {'l2','linf','l1'}")
+    return NORMS[norm]
+
+
+def _reject_out_of_regime(ok: np.ndarray, norm: str = "l2") -> None:
     if not ok.all():
         bad = int(np.flatnonzero(~ok)[0])
         raise NotImplementedError(
-            f"sequence {bad} is outside the closed form's regime (needs ||z_t|| <= 1 and "
-            "y_t = ±1); the general exact-FTL SOCP is out of scope")
+            f"sequence {bad} is outside the closed form's regime for the {norm} ball (needs "
+            f"{_DUAL.get(norm, norm)} and y_t = ±1); the general exact-FTL SOCP/LP is out "
+            "of scope")
 
 
 def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, device: int = 0,
                     check_regime: bool = True):
     """exact_ftl.py:280-333 (compute_prefix_actions + replay) for B sequences on the GPU,
-    in the closed form that is the exact SOCP solution when every ||z_t|| <= 1 and
-    y_t = ±1 (include/ocx.h, ocx_ftl_exact_batch).
+    over the unit ball of ``norm`` ('l2', 'l1', 'linf'), in the closed form that is the
+    exact SOCP / LP solution when every row's dual norm is <= 1 and y_t = ±1
+    (include/ocx.h, ocx_ftl_exact_batch).
 
     Returns (cum_loss [B], comp_loss [B], comparator actions[T] [B, d], in_regime [B]);
     with ``check_regime`` a sequence outside the regime raises NotImplementedError (the
-    general SOCP is out of scope: cvxpy is absent and its results are unpinned)."""
-    if norm not in NORMS:
-        raise NotImplementedError(f"exact FTL for norm={norm!r}: only 'l2' is provided")
+    general SOCP/LP is out of scope: cvxpy is absent and its results are unpinned)."""
+    code = _norm_code(norm)
     z = _f64(z)
     y = _f64(y)
     B, T, d = _check_zy(z, y)
@@ -131,12 +139,12 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, 
     comp = np.zeros(B)
     act = np.zeros((B, d))
     rg = np.zeros(B, dtype=np.int32)
-    _lib.call("ocx_ftl_exact_batch", ptr(z), ptr(y), B, T, d, NORMS[norm], ptr(cum), ptr(comp),
+    _lib.call("ocx_ftl_exact_batch", ptr(z), ptr(y), B, T, d, code, ptr(cum), ptr(comp),
               ptr(act), rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq),
               int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok)
+        _reject_out_of_regime(ok, norm)
     return cum, comp, act, ok
 
 
@@ -148,22 +156,22 @@ def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LAN
 
     Returns (actions, in_regime [B]); with ``check_regime`` a sequence outside the regime
     raises NotImplementedError."""
-    if norm not in NORMS:
-        raise NotImplementedError(f"exact FTL for norm={norm!r}: only 'l2' is provided")
+    code = _norm_code(norm)
     z = _f64(z)
     y = _f64(y)
     B, T, d = _check_zy(z, y)
     act = np.zeros((B, T + 1, d))
     rg = np.zeros(B, dtype=np.int32)
-    _lib.call("ocx_ftl_prefix_actions_batch", ptr(z), ptr(y), B, T, d, NORMS[norm], ptr(act),
+    _lib.call("ocx_ftl_prefix_actions_batch", ptr(z), ptr(y), B, T, d, code, ptr(act),
               rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok)
+        _reject_out_of_regime(ok, norm)
     return act, ok
 
 
-def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = LANES_BEST, device: int = 0,
+def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, norm: str = "l2",
+                        lanes_per_seq: int = LANES_BEST, device: int = 0,
                         check_regime: bool = True, with_ftl_comparator: bool = False):
     """exact_ftl_driver.py:157-186 for B sequences in one read of the data: exact FTL
     (closed form, as ftl_exact_batch) and FTRL against its comparator actions[T].
@@ -180,10 +188,11 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, lanes_per_seq: int = LANES
     rg = np.zeros(B, dtype=np.int32)
     _lib.call("ocx_ftrl_vs_exact_batch", ptr(z), ptr(y), B, T, d, float(eta0), ptr(cr), ptr(ce),
               ptr(cmp_e), ptr(cmp_f) if with_ftl_comparator else None, ptr(act),
-              rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
+              rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _norm_code(norm),
+              int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok)
+        _reject_out_of_regime(ok, norm)
     out = {"ftrl": cr - cmp_e, "exact": ce - cmp_e, "cum_ftrl": cr, "cum_exact": ce,
            "comp": cmp_e, "action": act, "in_regime": ok}
     if with_ftl_comparator:
@@ -373,7 +382,7 @@ class DeviceBatch:
         self._keep_th = self._hold(th)
         return self.regret
 
-    def ftl_exact(self, cmp_action=None, regime=None):
+    def ftl_exact(self, cmp_action=None, regime=None, norm: str = "l2"):
         """Exact FTL (l2 ball, closed form; see ftl_exact_batch) on the resident batch:
         self.cum / self.comp get the replay and comparator losses, ``cmp_action``
         [B, d] (device, optional) the exact comparator, ``regime`` [B] int32 the
@@ -382,14 +391,15 @@ class DeviceBatch:
         if regime is None:
             with self._on_stream():
                 regime = torch.zeros(max(self.L.B, 1), dtype=torch.int32, device=self.device)
-        _lib.call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(), 0,
+        _lib.call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+                  _norm_code(norm),
                   self.cum.data_ptr(), self.comp.data_ptr(),
                   cmp_action.data_ptr() if cmp_action is not None else None,
                   regime.data_ptr(), self._sp)
         return regime
 
     def ftrl_vs_exact(self, eta0: float = SQRT2, comp_ftl=None, cmp_action=None, regime=None,
-                      closed_comparator: Optional[bool] = None):
+                      closed_comparator: Optional[bool] = None, norm: str = "l2"):
         """ftrl_vs_exact_batch on the resident batch: self.cum gets FTRL's cumulative loss,
         self.comp the exact comparator's loss, self.cum_exact exact FTL's (allocated on first
         use); ``comp_ftl`` [B] (device, optional) the loss of FTL(theta_ftrl).  Returns the
@@ -409,7 +419,8 @@ class DeviceBatch:
                   float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
                   cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
-                  _lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0, self._sp)
+                  _norm_code(norm), _lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0,
+                  self._sp)
         return regime
 
     def max_regret(self, out=None):

@@ -4,21 +4,29 @@ imports): ``ExactFTLNoClip``, ``compute_prefix_actions``, ``replay_exact_ftl``,
 names, signatures and errors.  The FTRL loop (exact_ftl.py:230-277), the replay
 (:306-333) and the exact FTL solutions all run in the HIP kernels.
 
-Exact FTL (the cvxpy SOCP of ``ExactFTLNoClip``, exact_ftl.py:62-193) is solved on the
-GPU in closed form for the l2 ball whenever the data satisfy ||z_t|| <= 1 and
-y_t = ±1 — every sequence family and adversary of the reference does: there
-½Σ|z_i·x − y_i| = ½(t − x·S_t) on the ball, so the minimiser is S_t/||S_t||,
-S_t = Σ_{i<t} y_i z_i (engine.ftl_prefix_actions_batch / ftl_exact_batch).
+Exact FTL (the cvxpy SOCP / LP of ``ExactFTLNoClip``, exact_ftl.py:62-193) is solved on
+the GPU in closed form whenever every row's dual norm is <= 1 and y_t = ±1: then
+|z_i·x| <= 1 on the ball, ½Σ|z_i·x − y_i| = ½(t − x·S_t), S_t = Σ_{i<t} y_i z_i, and the
+minimiser maximises x·S_t over the ball (engine.ftl_prefix_actions_batch / ftl_exact_batch):
 
-* Degenerate prefixes (S_t = 0, e.g. the empty prefix): every point of the ball is
-  optimal; the engine returns 0 (cvxpy's interior-point choice is solver-dependent).
-* Outside that regime, and for the l1 / linf balls, the general SOCP/LP is out of scope
-  (DESIGN.md §7): those calls raise ``NotImplementedError``.  A caller can still pass
-  ``comparator_action`` / ``prefix_actions`` or any solver object with the reference's
-  methods (``reset_buffers`` / ``append_row`` / ``solve_prefix_from_full``).
-* Parity of the closed form against cvxpy is **unpinned**: cvxpy is absent here and the
-  reference ships no fixture for it.  It is checked against the C oracle's closed form
-  and independently against scipy SLSQP on the CPU (tests/test_exact_comparator_cpu.py).
+* l2 ball (regime ||z_t||_2 <= 1 — every sequence family and adversary of the reference):
+  S_t/||S_t||;
+* l1 ball (regime max_j |z_tj| <= 1 — implied by the l2 one, so again every family):
+  sign(S_j*) e_j* with j* the first coordinate of largest |S_j|;
+* linf ball (regime sum_j |z_tj| <= 1 — rows this small are rare in the reference's data):
+  sign(S_t) componentwise.
+
+* Degenerate prefixes (S_t = 0, e.g. the empty prefix; ties in |S_j| for l1; zero
+  coordinates of S_t for linf): the maximiser is not unique and cvxpy's choice is
+  solver-dependent; the engine returns the point above (0 where S_t = 0).
+* Outside the regime the general SOCP/LP is out of scope: those calls raise
+  ``NotImplementedError``.  A caller can still pass ``comparator_action`` /
+  ``prefix_actions`` or any solver object with the reference's methods
+  (``reset_buffers`` / ``append_row`` / ``solve_prefix_from_full``).
+* Parity of the closed forms against cvxpy is **unpinned**: cvxpy is absent here and the
+  reference ships no fixture for it.  They are checked against the oracle's restatement
+  and independently against scipy (SLSQP for l2, HiGHS LPs for l1 / linf) on the CPU
+  (tests/test_exact_comparator_cpu.py).
 """
 from __future__ import annotations
 
@@ -60,7 +68,7 @@ class ExactFTLNoClip:
     ``solver`` / ``solver_opts`` arguments are accepted and kept for signature parity
     (no cvxpy backend is involved).
 
-    ``norm='l2'`` only: 'linf' / 'l1' raise NotImplementedError, anything else
+    ``norm`` 'l2', 'l1' or 'linf' (closed forms, module docstring); anything else raises
     ValueError (exact_ftl.py:101-102)."""
 
     def __init__(self, d: int, T_max: int, *, norm: Literal["l2", "linf", "l1"] = "l2",
@@ -72,10 +80,6 @@ class ExactFTLNoClip:
         self.solver_opts = {} if solver_opts is None else dict(solver_opts)
         if norm not in _NORMS:
             raise ValueError("norm must be one of {'l2','linf','l1'}")
-        if norm != "l2":
-            raise NotImplementedError(
-                f"exact FTL over the {norm} ball (an LP in the reference) is out of scope; "
-                "only the l2 ball is solved (closed form on the GPU)")
         self._Z_buf = np.zeros((self.T_max, self.d), dtype=np.float64)
         self._y_buf = np.zeros(self.T_max, dtype=np.float64)
         self._w_buf = np.zeros(self.T_max, dtype=np.float64)

@@ -139,9 +139,70 @@ def replay_cum_loss(z, y, actions) -> float:
     return float(out[0])
 
 
-def ftl_exact_closed_form(z, y):
-    """exact_ftl.py:280-333 (l2 ball) in closed form → (cum_loss, comp_loss, actions[T],
-    in_regime).  See oc_ftl_exact in ocx_oracle.c."""
+def _poly_action(theta: np.ndarray, norm: str) -> np.ndarray:
+    """Exact FTL over the l1 / linf unit ball for theta = -S (exact_ftl.py:83-105 in its
+    linear regime): maximise x.S over the ball.  l1: sign(S_j*) e_j* at the FIRST largest
+    |S_j| (0 if S = 0); linf: sign(S) componentwise (0 where S_j = 0)."""
+    x = np.zeros_like(theta)
+    if norm == "linf":
+        x[theta > 0.0] = -1.0
+        x[theta < 0.0] = 1.0
+        return x
+    a = np.abs(theta)
+    j = int(np.argmax(a))            # first index of the maximum
+    if a[j] > 0.0:
+        x[j] = -1.0 if theta[j] > 0.0 else 1.0
+    return x
+
+
+def _dual_ok(zt: np.ndarray, norm: str) -> bool:
+    if norm == "l1":
+        return float(np.max(np.abs(zt), initial=0.0)) <= 1.0 + 1e-12
+    acc = 0.0
+    for v in zt:                     # sequential (the kernels' exact-mode order)
+        acc += abs(float(v))
+    return acc <= 1.0 + 1e-12
+
+
+def _seqdot(a: np.ndarray, b: np.ndarray) -> float:
+    acc = 0.0
+    for u, v in zip(a, b):           # fast_algorithms.py:11-16 order
+        acc += float(u) * float(v)
+    return acc
+
+
+def ftl_exact_poly(z, y, norm: str):
+    """exact_ftl.py:280-333 over the l1 / linf ball in closed form (pure Python loops, small
+    cases only) → (cum_loss, comp_loss, actions[T], in_regime, actions [T+1, d]).  The same
+    operation order as the kernels in exact mode: theta += -y_t z_t, x_t from theta,
+    q_t = z_t.x_t summed sequentially, the comparator loss in a second pass."""
+    z = _f64(z)
+    y = _f64(y)
+    T, d = z.shape
+    th = np.zeros(d)
+    acts = np.zeros((T + 1, d))
+    cum = 0.0
+    ok = True
+    for t in range(T):
+        x = _poly_action(th, norm)
+        acts[t] = x
+        cum += 0.5 * abs(_seqdot(z[t], x) - y[t])
+        ok = ok and _dual_ok(z[t], norm) and abs(y[t]) == 1.0
+        th = th + (-y[t]) * z[t]
+    xs = _poly_action(th, norm)
+    acts[T] = xs
+    comp = 0.0
+    for t in range(T):
+        comp += 0.5 * abs(_seqdot(z[t], xs) - y[t])
+    return cum, comp, xs, ok, acts
+
+
+def ftl_exact_closed_form(z, y, norm: str = "l2"):
+    """exact_ftl.py:280-333 in closed form → (cum_loss, comp_loss, actions[T], in_regime).
+    l2: oc_ftl_exact in ocx_oracle.c; l1 / linf: ftl_exact_poly."""
+    if norm != "l2":
+        cum, comp, xs, ok, _ = ftl_exact_poly(z, y, norm)
+        return cum, comp, xs, ok
     z = _f64(z)
     y = _f64(y)
     T, d = z.shape
@@ -153,9 +214,12 @@ def ftl_exact_closed_form(z, y):
     return float(out[0]), float(out[1]), a, bool(rg.value)
 
 
-def ftl_prefix_actions(z, y):
-    """exact_ftl.py:280-303 (l2 ball) in closed form → (actions [T+1, d], in_regime).
-    See oc_ftl_prefix_actions in ocx_oracle.c."""
+def ftl_prefix_actions(z, y, norm: str = "l2"):
+    """exact_ftl.py:280-303 in closed form → (actions [T+1, d], in_regime).
+    l2: oc_ftl_prefix_actions in ocx_oracle.c; l1 / linf: ftl_exact_poly."""
+    if norm != "l2":
+        _, _, _, ok, acts = ftl_exact_poly(z, y, norm)
+        return acts, ok
     z = _f64(z)
     y = _f64(y)
     T, d = z.shape

@@ -1,10 +1,10 @@
 """The exact-FTL comparator (exact_ftl.py:62-193 solves it with cvxpy, absent here):
-validate the closed form the engine uses against an INDEPENDENT solver (scipy SLSQP on
-the SOCP epigraph).  Parity with the reference's cvxpy path is unpinned; this pins the
-mathematics.  CPU only."""
+validate the closed forms the engine uses against INDEPENDENT solvers (scipy SLSQP on the
+l2 SOCP epigraph; scipy HiGHS on the l1 / linf LPs).  Parity with the reference's cvxpy
+path is unpinned; this pins the mathematics.  CPU only."""
 import numpy as np
 import pytest
-from scipy.optimize import minimize
+from scipy.optimize import linprog, minimize
 
 from oracle import oracle as O
 
@@ -65,3 +65,61 @@ def test_regime_flag():
     assert O.ftl_exact_closed_form(z, y)[3]
     assert not O.ftl_exact_closed_form(2.0 * z, y)[3]         # rows outside the ball
     assert not O.ftl_exact_closed_form(z, 0.5 * y)[3]         # labels not ±1
+
+
+def lp_solve(z, y, norm):
+    """min_x 0.5*sum|z_i.x - y_i| s.t. ||x||_norm <= 1 (exact_ftl.py:83-105 'l1' / 'linf')
+    as an LP over (u, v, s) with x = u - v, u, v >= 0, s >= |z x - y| (HiGHS)."""
+    T, d = z.shape
+    c = np.r_[np.zeros(2 * d), 0.5 * np.ones(T)]
+    A = np.block([[z, -z, -np.eye(T)], [-z, z, -np.eye(T)]])
+    b = np.r_[y, -y]
+    if norm == "l1":
+        A = np.vstack([A, np.r_[np.ones(2 * d), np.zeros(T)]])
+        b = np.r_[b, 1.0]
+        bounds = [(0, None)] * (2 * d + T)
+    else:
+        bounds = [(0, 1)] * (2 * d) + [(0, None)] * T
+    res = linprog(c, A_ub=A, b_ub=b, bounds=bounds, method="highs")
+    assert res.status == 0
+    return res.x[:d] - res.x[d:2 * d], res.fun
+
+
+@pytest.mark.parametrize("norm", ["l1", "linf"])
+@pytest.mark.parametrize("seed,T,d", [(0, 30, 3), (1, 40, 5), (2, 25, 8), (3, 60, 2)])
+def test_poly_closed_form_is_the_lp_minimiser(norm, seed, T, d):
+    """l1 / linf balls: in the dual-norm regime the closed form's objective equals the LP
+    optimum (HiGHS), every prefix action is a prefix minimiser, and the action is the LP's
+    wherever the maximiser is unique."""
+    rng = np.random.default_rng(100 + seed)
+    z = rng.standard_normal((T, d))
+    if norm == "l1":
+        z /= np.maximum(1.0, np.abs(z).max(axis=1, keepdims=True))   # max_j |z_j| <= 1
+    else:
+        z /= np.maximum(1.0, np.abs(z).sum(axis=1, keepdims=True))   # sum_j |z_j| <= 1
+    y = np.where(rng.random(T) < 0.5, -1.0, 1.0)
+    cum, comp, act, ok, acts = O.ftl_exact_poly(z, y, norm)
+    assert ok
+    x_lp, f_lp = lp_solve(z, y, norm)
+    assert abs(comp - f_lp) < 1e-8
+    assert abs(objective(z, y, act) - comp) < 1e-12
+    S = (y[:, None] * z).sum(axis=0)
+    unique = (np.all(S != 0.0) if norm == "linf"
+              else np.sum(np.abs(S) == np.abs(S).max()) == 1 and np.abs(S).max() > 0)
+    if unique:
+        assert np.allclose(act, x_lp, atol=1e-7)
+    for t in (1, T // 2, T - 1):
+        _, f_t = lp_solve(z[:t], y[:t], norm)
+        assert abs(objective(z[:t], y[:t], acts[t]) - f_t) < 1e-8, t
+    # the closed form of the comparator loss: T/2 - max_x x.S / 2
+    best = np.abs(S).max() if norm == "l1" else np.abs(S).sum()
+    assert comp == pytest.approx(0.5 * (T - best), abs=1e-10)
+
+
+def test_poly_regime_flags():
+    z, y = O.gT_sample(1, 20, 0, 3)                 # ||z||_2 <= 1 implies max |z_j| <= 1
+    assert O.ftl_exact_poly(z, y, "l1")[3]
+    assert not O.ftl_exact_poly(2.0 * z, y, "l1")[3]
+    assert not O.ftl_exact_poly(z, y, "linf")[3]    # sum |z_j| > 1 for clipped rows
+    assert O.ftl_exact_poly(z / 3.0, y, "linf")[3]
+    assert not O.ftl_exact_poly(z / 3.0, 0.5 * y, "linf")[3]

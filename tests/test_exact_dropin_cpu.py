@@ -52,9 +52,8 @@ def test_solver_norms():
     from online_convex_optimization_amd.exact_ftl import ExactFTLNoClip
     with pytest.raises(ValueError):
         ExactFTLNoClip(3, 4, norm="l3")
-    for norm in ("l1", "linf"):  # LPs in the reference: out of scope here
-        with pytest.raises(NotImplementedError):
-            ExactFTLNoClip(3, 4, norm=norm)
+    for norm in ("l1", "linf"):  # LPs in the reference: closed forms in their regime
+        assert ExactFTLNoClip(3, 4, norm=norm).norm == norm
 
 
 def test_compute_prefix_actions_argument_checks():

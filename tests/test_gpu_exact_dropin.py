@@ -113,3 +113,62 @@ def test_prefix_actions_batch_lane_splits(ef):
                 continue
             acts, ok = engine.ftl_prefix_actions_batch(z, y, lanes_per_seq=P)
             assert ok.all() and np.array_equal(acts, want), (B, T, d, P)
+
+
+# ------------------------------------------------------------------ l1 / linf balls
+def _poly_data(rng, B, T, d, norm):
+    z = rng.standard_normal((B, T, d))
+    if norm == "l1":
+        z /= np.maximum(1.0, np.abs(z).max(axis=2, keepdims=True))
+    else:
+        z /= np.maximum(1.0, np.abs(z).sum(axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    return z, y
+
+
+@pytest.mark.parametrize("norm", ["l1", "linf"])
+def test_poly_exact_ftl_matches_oracle(ef, norm):
+    """Exact FTL over the l1 / linf ball (closed forms, include/ocx.h ocx_ftl_exact_batch):
+    prefix actions, replay losses and the comparator action bit-identical to the oracle in
+    exact mode, on every lane split; the fused FTRL-vs-exact kernel agrees too."""
+    from online_convex_optimization_amd import engine
+    rng = np.random.default_rng(11 if norm == "l1" else 12)
+    for B, T, d in ((17, 120, 5), (9, 60, 64), (3, 30, 300)):
+        z, y = _poly_data(rng, B, T, d, norm)
+        ref = [O.ftl_exact_poly(z[b], y[b], norm) for b in range(B)]
+        assert all(r[3] for r in ref)
+        for P in (1, -1, -4, 4):
+            if P != 1 and d > 64 * abs(P):
+                continue
+            cum, comp, act, ok = engine.ftl_exact_batch(z, y, norm=norm, lanes_per_seq=P)
+            acts, ok2 = engine.ftl_prefix_actions_batch(z, y, norm=norm, lanes_per_seq=P)
+            assert ok.all() and ok2.all()
+            want_acts = np.stack([r[4] for r in ref])
+            assert np.array_equal(acts, want_acts), (B, T, d, P)
+            assert np.array_equal(act, want_acts[:, -1]), (B, T, d, P)
+            wc = np.array([r[0] for r in ref])
+            wp = np.array([r[1] for r in ref])
+            if P in (1, -1, -4):   # sequential sums: bit for bit
+                assert np.array_equal(cum, wc) and np.array_equal(comp, wp), (B, T, d, P)
+            else:
+                assert np.allclose(cum, wc, rtol=1e-12, atol=1e-12)
+                assert np.allclose(comp, wp, rtol=1e-12, atol=1e-12)
+            r = engine.ftrl_vs_exact_batch(z, y, SQ2, norm=norm, lanes_per_seq=P)
+            assert r["in_regime"].all() and np.array_equal(r["action"], act)
+            assert np.allclose(r["cum_exact"], wc, rtol=1e-12, atol=1e-12)
+            assert np.allclose(r["comp"], wp, rtol=1e-12, atol=1e-12)
+        # the drop-in solver object and run_ftl_exact
+        s = ef.ExactFTLNoClip(d=d, T_max=T, norm=norm)
+        a0 = ef.compute_prefix_actions(s, z[0], y[0])
+        assert np.array_equal(a0, ref[0][4])
+        res = ef.run_ftl_exact(z[0], y[0], norm=norm)
+        assert (res.cum_loss, res.comp_loss) == (ref[0][0], ref[0][1])
+
+
+def test_poly_out_of_regime_rejected(ef):
+    z, y, _ = O.random_iid_sample(2025, 50, 0)     # ||z_t||_2 <= 1: inside l1, not linf
+    ef.run_ftl_exact(z, y, norm="l1")
+    with pytest.raises(NotImplementedError):
+        ef.run_ftl_exact(z, y, norm="linf")
+    with pytest.raises(NotImplementedError):
+        ef.run_ftl_exact(3.0 * z, y, norm="l1")
