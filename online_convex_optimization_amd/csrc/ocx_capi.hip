@@ -718,6 +718,8 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     if (int rc = ocx_layout_init(R % Bc ? R % Bc : Bc, 1, d, lanes_per_seq, &Ltail)) return rc;
     OCX_HIP(cx->theta.ensure((size_t)std::max(Bc * L1.Dp, Ltail.B * Ltail.Dp) * 8));
     OCX_HIP(cx->acc.ensure((size_t)(Bc * 4 + 1) * 8));
+    int64_t unclean_every = 0;
+    if (const char* e = std::getenv("OCX_TEST_UNCLEAN_EVERY")) unclean_every = std::atoll(e);
     for (int64_t r0 = 0; r0 < R; r0 += Bc) {
         const int64_t nb = std::min(Bc, R - r0);
         ocx_layout Lb;
@@ -733,6 +735,14 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
         OCX_HIP(hipMemsetAsync(th, 0, (size_t)nb * Lb.Dp * 8, st));
         OCX_HIP(hipMemsetAsync(cum, 0, (size_t)Bc * 2 * 8, st));
         if (unclean) OCX_HIP(hipMemsetAsync(unclean, 0, (size_t)(nb + 1) * 8, st));
+        if (unclean && unclean_every > 0) {
+            // test knob (OCX_TEST_UNCLEAN_EVERY=k): mark runs r0 + b with b % k == 0 as if a
+            // step had failed the closed form's check, so the second pass serves them
+            std::vector<double> mk((size_t)nb, 0.0);
+            for (int64_t i = 0; i < nb; i += unclean_every) mk[(size_t)i] = 1.0;
+            OCX_HIP(hipMemcpyAsync(unclean, mk.data(), (size_t)nb * 8, hipMemcpyHostToDevice, st));
+            OCX_HIP(hipStreamSynchronize(st));
+        }
         for (int pass = 0; pass < 2; ++pass) {
             if (pass == 1 && unclean) {
                 // closed-form comparator for the clean sequences (no regeneration); the

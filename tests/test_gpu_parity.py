@@ -615,3 +615,29 @@ def test_ftrl_vs_exact_closed_form(ocx, P):
     a, bb = a.cpu().numpy(), pk.comp.cpu().numpy()
     assert a[3] == bb[3] and a[50] == bb[50]
     assert close_closed(bb, a, 120)
+
+
+@pytest.mark.parametrize("P", [0, 128])
+def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
+    """The streamed path's closed form (ocx_alg_chunk_kernel mode 2) and its fallback: with
+    every third run marked as failing the check (OCX_TEST_UNCLEAN_EVERY, a test knob), those
+    runs get the regenerated second pass, bit-identical to the resident two-pass kernel; the
+    rest keep the closed form, bit-identical to the resident closed form."""
+    import torch
+    eng = ocx["engine"]
+    T, d, runs = 257, 64, 40
+    db = eng.DeviceBatch(runs, T, d, lanes_per_seq=P).generate_gT(base_seed=4, run0=7)
+    closed = db.simulate_alg().clone()
+    two = db.simulate_alg(closed_comparator=False).clone()
+    torch.cuda.synchronize()
+    closed, two = closed.cpu().numpy(), two.cpu().numpy()
+    del db
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(200e3 / 2**30))  # ~200 KB → streamed
+    monkeypatch.setenv("OCX_MIN_RESIDENT", str(1 << 30))
+    plain = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
+    assert np.array_equal(plain, closed)
+    monkeypatch.setenv("OCX_TEST_UNCLEAN_EVERY", "3")
+    mixed = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
+    marked = np.arange(runs) % 3 == 0
+    assert np.array_equal(mixed[marked], two[marked])
+    assert np.array_equal(mixed[~marked], closed[~marked])
