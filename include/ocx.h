@@ -245,6 +245,12 @@ int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const doub
  * theta_e = -S_T is in registers), so such waves read z once instead of twice; the rest
  * stream the second pass.  Equal to the sequential sums up to their rounding. */
 #define OCX_ALG_CLOSED_COMPARATOR 2
+/* OCX_ALG_TREE_SUMS (ocx_dev_ftrl_vs_exact_ex): butterfly sums even when the layout chains
+ * (the tiling is the same): the fused kernel's four chained totals per step leave it
+ * latency-bound where the plain FTRL kernel streams (32768 x 1e4 x 64, one pass: 43 ms
+ * chained vs 28 ms butterfly); about 1e-16 relative instead of the sequential order.
+ * ocx_ftrl_vs_exact_batch applies it for lanes_per_seq = OCX_LANES_BEST. */
+#define OCX_ALG_TREE_SUMS 4
 int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                              double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                              double* comp_ftl, double* cmp_action, int32_t* regime, int norm,

@@ -86,6 +86,7 @@ SIGNATURES = {
 }
 OCX_ALG_CLIPPED_ROWS = 1
 OCX_ALG_CLOSED_COMPARATOR = 2
+OCX_ALG_TREE_SUMS = 4
 
 _lib = None
 _lock = threading.Lock()

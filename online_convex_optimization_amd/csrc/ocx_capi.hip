@@ -348,11 +348,15 @@ int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const d
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (L->B && (!cum_ftrl || !cum_exact || !comp_exact || !regime))
         return fail(OCX_E_INVALID, "NULL output buffer");
-    if (flags & ~(OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR))
+    if (flags & ~(OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR | OCX_ALG_TREE_SUMS))
         return fail(OCX_E_INVALID, "unknown flags");
-    OCX_HIP(ocx_launch_ftrl_exact(L, z_tiled, y_tiled, eta0, cum_ftrl, cum_exact, comp_exact,
+    ocx_layout Lt = *L;
+    if (flags & OCX_ALG_TREE_SUMS) Lt.chain = 0;  // same tiling, butterfly sums
+    OCX_HIP(ocx_launch_ftrl_exact(&Lt, z_tiled, y_tiled, eta0, cum_ftrl, cum_exact, comp_exact,
                                   comp_ftl, cmp_action, regime, (hipStream_t)stream,
-                                  flags ? 1 : 0, norm));
+                                  (flags & (OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR)) ? 1
+                                                                                             : 0,
+                                  norm));
     return OCX_OK;
 }
 
@@ -563,8 +567,10 @@ int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t
     double* o = cx->out.as<double>();
     int* rg = reinterpret_cast<int*>(o + B * (4 + d));
     // outside the bit-exact modes the comparator losses take their closed form where the
-    // kernel certifies the regime (ocx_dev_ftrl_vs_exact_ex)
+    // kernel certifies the regime, and OCX_LANES_BEST sums with the butterfly
+    // (ocx_dev_ftrl_vs_exact_ex, OCX_ALG_TREE_SUMS)
     const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
+    if (lanes_per_seq == OCX_LANES_BEST) L.chain = 0;
     OCX_HIP(ocx_launch_ftrl_exact(&L, cx->zt.as<double>(), cx->yt.as<double>(), eta0, o, o + B,
                                   o + 2 * B, comp_ftl ? o + 3 * B : nullptr, o + 4 * B, rg, st,
                                   onepass, norm));

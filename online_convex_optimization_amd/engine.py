@@ -265,6 +265,7 @@ class DeviceBatch:
         self.L = _lib.layout(B, T, d, lanes_per_seq)
         # bit-exact modes keep the reference's two-pass comparator sum (see simulate_alg)
         self.exact = lanes_per_seq == LANES_EXACT or lanes_per_seq < 0
+        self.best = lanes_per_seq == LANES_BEST
         self.rows_clipped = False  # set by generate_gT: every ||z_t|| <= 1
         self.device = torch.device("cuda", device)
         with torch.cuda.device(self.device):
@@ -405,7 +406,8 @@ class DeviceBatch:
         use); ``comp_ftl`` [B] (device, optional) the loss of FTL(theta_ftrl).  Returns the
         regime flags.  ``closed_comparator`` (default: not a bit-exact layout) takes both
         comparator losses in closed form for the sequences the kernel finds in the unit-ball
-        regime (ocx_dev_ftrl_vs_exact_ex): one HBM pass instead of two."""
+        regime (ocx_dev_ftrl_vs_exact_ex): one HBM pass instead of two.  Under
+        OCX_LANES_BEST the kernel sums with the butterfly (OCX_ALG_TREE_SUMS)."""
         torch = self.torch
         n = max(self.L.B, 1)
         with self._on_stream():
@@ -415,12 +417,16 @@ class DeviceBatch:
                 regime = torch.zeros(n, dtype=torch.int32, device=self.device)
         if closed_comparator is None:
             closed_comparator = not self.exact
+        flags = _lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0
+        if self.best and self.L.chain:
+            # OCX_LANES_BEST: chained totals leave this kernel latency-bound (43 vs 28 ms at
+            # 32768 x 1e4 x 64, profiles/r02_fused_exact_lanes.jsonl): butterfly sums instead
+            flags |= _lib.OCX_ALG_TREE_SUMS
         _lib.call("ocx_dev_ftrl_vs_exact_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
                   cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
-                  _norm_code(norm), _lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0,
-                  self._sp)
+                  _norm_code(norm), flags, self._sp)
         return regime
 
     def max_regret(self, out=None):

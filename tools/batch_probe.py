@@ -17,9 +17,14 @@ def main():
         db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes)
         res = {"B": B, "T": T, "d": d, "lanes": lanes, "P": int(db.L.P), "C": int(db.L.C),
                "chain": int(db.L.chain), "waves": int(db.L.G)}
-        for name, fn in (("gen_ms", lambda: db.generate_gT(0, 0)),
-                         ("sim_closed_ms", lambda: db.simulate_alg(closed_comparator=True)),
-                         ("sim_two_pass_ms", lambda: db.simulate_alg(closed_comparator=False))):
+        fns = [("gen_ms", lambda: db.generate_gT(0, 0)),
+               ("sim_closed_ms", lambda: db.simulate_alg(closed_comparator=True)),
+               ("sim_two_pass_ms", lambda: db.simulate_alg(closed_comparator=False))]
+        if os.environ.get("PROBE_EXACT"):  # the fused FTRL + exact FTL kernel (configs[2])
+            cf = torch.zeros(B, dtype=torch.float64, device=db.device)
+            fns += [("fe_closed_ms", lambda: db.ftrl_vs_exact(comp_ftl=cf, closed_comparator=True)),
+                    ("fe_two_pass_ms", lambda: db.ftrl_vs_exact(comp_ftl=cf, closed_comparator=False))]
+        for name, fn in fns:
             fn()
             torch.cuda.synchronize()
             e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
