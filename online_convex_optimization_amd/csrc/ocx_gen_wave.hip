@@ -19,6 +19,7 @@
 // every round, and a batch of a few thousand sequences already fills the GPU.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "ocx_internal.h"
 #include "ocx_rng.h"
@@ -758,17 +759,30 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
     // the kernel counts a sequence's normals in 32 bits
     if ((MODE == 0 ? T : T_seed) * d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
     if (d == 64 && (MODE == 1 || (int64_t)P * C == 64)) {
-        // Few streams (the capacity-limited T = 1e5 batch): the default form's 4 waves per
-        // SIMD would give each wave two or more whole sequences while half the wave slots
-        // stay empty; the low-LDS form's 6 waves per SIMD give every stream its own wave
-        // (d = 64, T = 1e5, 4900 streams: 161 -> 117 ms).  Beyond that the default form is
-        // faster (32768 x 1e4: 77.9 vs 82.7 ms at 6 waves; profiles/r02_gen_ring640_probe.jsonl).
+        // Two forms: the default (8-row batches, 4 waves per SIMD: its 8 KB ring fills the
+        // LDS) and the low-LDS one (7-row batches, 6 waves per SIMD).  Every wave takes
+        // ceil(streams / slots) whole streams, so a form's makespan is that count times the
+        // waves of its busiest SIMD; the low-LDS form wins where that is smaller, or equal
+        // within the ~6 % its extra waves buy per stream when it really runs more waves per
+        // SIMD (1e6 x T=100: 23.9 vs 25.3 ms; 131072 x 1e3: 30.4 vs 31.4; 4900 x 1e5: 117 vs
+        // 161), and loses where its rounding is worse (32768 x 1e4: 78.9 vs 75.6 ms;
+        // profiles/r02_gen_forms.jsonl).
         int dev = 0, cus = 256;
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
-        if (MODE == 0 && nseq > (int64_t)cus * 16 && nseq <= (int64_t)cus * 24)
+        const int64_t simds = 4 * (int64_t)cus;
+        auto load = [&](int64_t w, int64_t& wps) {  // makespan in stream units, waves/SIMD
+            const int64_t per_wave = (nseq + w * simds - 1) / (w * simds);
+            const int64_t nw = (nseq + per_wave - 1) / per_wave;
+            wps = (nw + simds - 1) / simds;
+            return per_wave * wps;
+        };
+        int64_t wps4 = 0, wps6 = 0;
+        const int64_t l4 = load(4, wps4), l6 = load(6, wps6);
+        bool lr = l6 < l4 || (wps6 > wps4 && (double)l6 <= 1.06 * (double)l4);
+        if (MODE == 0 && lr)
             return launch_wave_df<MODE, 64, true>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G,
                                                   zt, ytl, st_in, st_out, lab_in, lab_out, st);
         return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,

@@ -166,6 +166,28 @@ def test_device_generator_matches_numpy(ocx, B, T, d, P):
     assert np.count_nonzero(zt) <= B * T * d
 
 
+@pytest.mark.parametrize("B,T", [(33, 20), (192, 2000), (5000, 40)])
+def test_generator_forms_agree(ocx, monkeypatch, B, T):
+    """The d = 64 generator's two forms (8-row batches / 4 waves per SIMD, and the
+    low-LDS 7-row form at 6 waves; ocx_gen_wave.hip launch_wave picks by makespan) write
+    the same tiles bit for bit, equal to NumPy's streams."""
+    import torch
+    eng = ocx["engine"]
+    out = {}
+    for form in ("default", "lr"):
+        monkeypatch.setenv("OCX_GEN_FORM", form)
+        db = eng.DeviceBatch(B, T, 64, lanes_per_seq=1).generate_gT(base_seed=3, run0=1)
+        torch.cuda.synchronize()
+        out[form] = (db.z.cpu().numpy(), db.y.cpu().numpy(), db.L)
+        del db
+    assert np.array_equal(out["default"][0], out["lr"][0])
+    assert np.array_equal(out["default"][1], out["lr"][1])
+    z = untile_z(out["lr"][0], out["lr"][2])
+    for b in (0, B // 2, B - 1):
+        zr, yr = O.gT_sample(3, T, 1 + b, 64)
+        assert np.array_equal(z[b], zr), b
+
+
 # ------------------------------------------------------------------ batched, all splits
 @pytest.mark.parametrize("T,d", [(300, 64), (200, 16), (50, 5), (40, 1024), (0, 7), (25, 1),
                                  (64, 100)])
