@@ -290,6 +290,29 @@ def test_full_size_properties(ocx):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("B,T,d", [(65536, 1000, 16), (512, 10000, 1024)])
+def test_config_shapes_full_size(ocx, B, T, d):
+    """configs[1] (65 536 sequences, d=16, T=1e3) and configs[4]'s shape (d=1024, T=1e4) at
+    full size: the default (BEST + closed-form comparator) and the bit-exact mode agree within
+    the closed form's bar, and sampled sequences match the oracle (bit for bit in exact
+    mode)."""
+    import torch
+    eng = ocx["engine"]
+    ex = eng.DeviceBatch(B, T, d, lanes_per_seq=1).generate_gT(base_seed=2, run0=0)
+    r_ex = ex.simulate_alg().clone()
+    del ex
+    best = eng.DeviceBatch(B, T, d).generate_gT(base_seed=2, run0=0)
+    r_best = best.simulate_alg().clone()
+    torch.cuda.synchronize()
+    del best
+    torch.cuda.empty_cache()
+    r_ex, r_best = r_ex.cpu().numpy(), r_best.cpu().numpy()
+    assert close_closed(r_best, r_ex, T)
+    for b in (0, 1, B // 3, B - 1):
+        z, y = O.gT_sample(2, T, b, d)
+        assert r_ex[b] == O.simulate_alg(z, y, 0, SQ2), b
+
+
 # ------------------------------------------------------------------ sequence families
 @pytest.mark.parametrize("family,runs,reps,T", [("iid", 48, 16, 1000), ("massart", 48, 20, 300),
                                                 ("iid", 3, 2, 100), ("massart", 2, 3, 1000)])
