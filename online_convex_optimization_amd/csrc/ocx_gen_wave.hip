@@ -193,7 +193,9 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 // One round: speculate 64 draws, parse them in stream order, append at most `need`
 // normals to the ring at `head` (when RING).  Returns the number appended and advances
 // the stream past exactly the draws those normals consumed (NumPy random_standard_normal).
-template <bool RING>
+// FULL: need == 64 is known (every round of a d = 64 row stream but the last): a rejection
+// round then appends at most 63 normals, so the need-capping tail below drops out.
+template <bool RING, bool FULL = false>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
     const ocx_u128 s = mul_add_u128(w.Ak, w.base, w.Dk);
@@ -211,7 +213,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const bool fast = rabs < tb.ki[idx];
 #endif
     const uint64_t rej = ballot(!fast);
-    if (rej == 0 && need == 64) {  // every draw accepted (64 % of rounds)
+    if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
         if (RING) ring[(head + (unsigned)lane) & rmask] = x;
         w.base = rl128(s, 63);
         return 64;
@@ -264,7 +266,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     uint64_t emit = (~rej | (rej & wacc)) & ~cons & lowmask(limit);
     int n = __builtin_popcountll(emit);
     int m = limit;  // draws consumed
-    if (n >= need) {
+    if (!FULL && n >= need) {
         int p;  // lane of the need-th normal
         if (n == need) {
             p = 63 - __builtin_clzll(emit);
@@ -526,6 +528,48 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
         ws_set(w, g0, Gk);
 
         // ---- rows
+        if constexpr (MODE == 0 && DF == 64) {
+            // d = 64: lean bookkeeping (the generic loop below spends scalar instructions on
+            // partial/ready counters every round): head − tailp normals wait in the ring, a
+            // batch of R rows leaves as soon as it is complete (at most one per round: the
+            // ring never holds more than R rows + 63), the rest after the last round
+            const uint32_t total = (uint32_t)(T * 64);
+            uint32_t produced = 0;
+            unsigned head = 0, tailp = 0;
+            int64_t t = 0;
+            while (produced < total) {
+                const uint32_t left = total - produced;
+                const int n = left >= 64u
+                                  ? zig_round<true, true>(w, 64, tb, ring, rmask, head, lane)
+                                  : zig_round<true>(w, (int)left, tb, ring, rmask, head, lane);
+                produced += (uint32_t)n;
+                head += (unsigned)n;
+                const unsigned pending = head - tailp;
+                if (pending >= (unsigned)(R * 64) || (produced == total && pending > 0)) {
+                    const int nrows = (int)(pending >> 6) < R ? (int)(pending >> 6) : R;
+                    // lanes 8r..8r+7: row r's NumPy pairwise sum of squares, its clip scale
+                    const double ss =
+                        leaf_sumsq<64>(ring, rmask, tailp + (unsigned)((lane >> 3) * 64), 64, lane);
+                    const double nrm = sqrt(ss);
+                    const double sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
+                    double* zp = zt + zoff + t * 128;
+                    // lane j stores coordinate j of each row: the default form's batches
+                    // start at multiples of 512 of its 1024 ring (one base, immediate
+                    // offsets); the low-LDS form's 7-row batches wrap the 512 ring
+                    const unsigned base = tailp & (unsigned)rmask;
+                    for (int r = 0; r < nrows; ++r) {
+                        const double scr = __hiloint2double(
+                            __builtin_amdgcn_readlane(__double2hiint(sc), r * 8),
+                            __builtin_amdgcn_readlane(__double2loint(sc), r * 8));
+                        const unsigned ro = LR ? ((tailp + 64u * (unsigned)r) & (unsigned)rmask)
+                                               : base + 64u * (unsigned)r;
+                        OCX_GEN_STORE(ring[ro + (unsigned)lane] * scr, zp + r * 128);
+                    }
+                    tailp += (unsigned)(nrows * 64);
+                    t += nrows;
+                }
+            }
+        } else {
         const int64_t rows = (MODE == 0) ? T : T_seed;
         uint32_t remaining = (uint32_t)(rows * d);  // normals still to draw (< 2^32, host-checked)
         unsigned head = 0, tailp = 0;  // ring counters (mod 2^32; masked on use)
@@ -659,6 +703,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
                 ready -= nrows;
             }
         }
+        }  // generic row loop
         if (MODE == 1) {
             if (lane == 0) save_state6(lab_out + 6 * b, w.base, w.inc, 0, 0);
             continue;
