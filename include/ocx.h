@@ -173,6 +173,23 @@ int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t b
                          int64_t d, double eta0, const int* devices, int ndev, int lanes_per_seq,
                          double* gmax, double* regrets);
 
+/* ---- float32 twin (algorithms.py, the module driver.py imports) ----------- */
+/* algorithms.py:28-54 simulate_alg (algo 0 FTRL, 1 FTL) and :65-120 simulate_SMART_like
+ * (algo 2, thresh[B] = theta_thresh per sequence), batched over B sequences of float32 rows
+ * z[B][T][d], y[B][T], d <= 32, in NumPy 2's float32 arithmetic:
+ * result[b] = the twin's np.float32 return value; cum_loss (double, the Python float
+ * accumulator), comp_loss (float32) and switch_step (SMART: step of the switch, -1 if none)
+ * are optional. */
+int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64_t d, int algo,
+                     double eta0, const double* thresh, float* result, double* cum_loss,
+                     float* comp_loss, int64_t* switch_step, int device);
+/* The float32 twin's g(T) inner loop (algorithms.py:150-169): the regrets of runs
+ * run0 .. run0+R-1 of _rng(base_seed, T, run), rows rounded to float32 and clipped in
+ * float32, FTRL with eta0; on device (generator + twin kernel), nothing but the regrets
+ * crosses PCIe. */
+int ocx_twin32_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                          double eta0, float* regrets, int device);
+
 /* ---- device entry points (tiled layout, caller-owned device memory) ------ */
 
 /* Re-tile device arrays z [B][T][d], y [B][T] into the layout. */

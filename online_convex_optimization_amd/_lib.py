@@ -22,6 +22,7 @@ c_u64 = ctypes.c_uint64
 c_int = ctypes.c_int
 c_double = ctypes.c_double
 c_vp = ctypes.c_void_p
+c_fp = ctypes.POINTER(ctypes.c_float)
 
 
 class OCXError(RuntimeError):
@@ -83,6 +84,9 @@ SIGNATURES = {
     "ocx_gT_sweep": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double, c_int, c_dp, c_dp]),
     "ocx_gT_sweep_devices": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double,
                                      ctypes.POINTER(c_int), c_int, c_int, c_dp, c_dp]),
+    "ocx_twin32_batch": (c_int, [c_fp, c_fp, c_i64, c_i64, c_i64, c_int, c_double, c_dp, c_fp,
+                                 c_dp, c_fp, c_i64p, c_int]),
+    "ocx_twin32_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_fp, c_int]),
 }
 OCX_ALG_CLIPPED_ROWS = 1
 OCX_ALG_CLOSED_COMPARATOR = 2

@@ -830,4 +830,85 @@ int ocx_gT_sweep(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed
                                 OCX_LANES_BEST, gmax, regrets);
 }
 
+// ---------------------------------------------------------------- float32 twin
+int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64_t d, int algo,
+                     double eta0, const double* thresh, float* result, double* cum_loss,
+                     float* comp_loss, int64_t* switch_step, int device) {
+    if (algo < 0 || algo > 2) return fail(OCX_E_INVALID, "algo must be 0 (FTRL), 1 (FTL) or 2 (SMART)");
+    if (B < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative size");
+    if (d > 32) return fail(OCX_E_UNSUPPORTED, "the float32 twin supports d <= 32");
+    ocx_layout L;
+    if (int rc = ocx_layout_init(B, T, d, -1, &L)) return rc;  // one lane per sequence
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || !result || (algo == 2 && !thresh))
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T);
+    OCX_HIP(cx->zraw.ensure(nz * 4));
+    OCX_HIP(cx->yraw.ensure(ny * 4));
+    OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+    OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+    OCX_HIP(cx->out.ensure((size_t)B * 16));
+    OCX_HIP(cx->sw.ensure((size_t)B * 8));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 4, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 4, hipMemcpyHostToDevice, st));
+    const double* dthr = nullptr;
+    if (algo == 2) {
+        OCX_HIP(cx->thr.ensure((size_t)B * 8));
+        OCX_HIP(hipMemcpyAsync(cx->thr.p, thresh, (size_t)B * 8, hipMemcpyHostToDevice, st));
+        dthr = cx->thr.as<double>();
+    }
+    OCX_HIP(ocx_launch_pack32(&L, cx->zraw.as<float>(), cx->yraw.as<float>(), cx->zt.as<double>(),
+                              cx->yt.as<double>(), st));
+    double* cum = cx->out.as<double>();
+    float* res = reinterpret_cast<float*>(cum + B);
+    float* comp = res + B;
+    OCX_HIP(ocx_launch_twin32(&L, cx->zt.as<double>(), cx->yt.as<double>(), algo, eta0, dthr, 0,
+                              res, cum, comp, cx->sw.as<int64_t>(), st));
+    OCX_HIP(hipMemcpyAsync(result, res, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    if (cum_loss) OCX_HIP(hipMemcpyAsync(cum_loss, cum, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    if (comp_loss) OCX_HIP(hipMemcpyAsync(comp_loss, comp, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    if (switch_step)
+        OCX_HIP(hipMemcpyAsync(switch_step, cx->sw.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
+int ocx_twin32_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                          double eta0, float* regrets, int device) {
+    if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
+    if (d > 32) return fail(OCX_E_UNSUPPORTED, "the float32 twin supports d <= 32");
+    if (T * d >= ((int64_t)1 << 32)) return fail(OCX_E_UNSUPPORTED, "T * d >= 2^32");
+    if (R == 0) return OCX_OK;
+    if (!regrets) return fail(OCX_E_INVALID, "NULL regrets");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    ocx_layout L1;
+    if (int rc = ocx_layout_init(1, T, d, -1, &L1)) return rc;
+    // batches of <= 4 GiB of tiles (raw float64 normals, rounded to float in the kernel)
+    const int64_t per_seq = std::max<int64_t>(8, T * (L1.C + 1) * 8);
+    const int64_t chunk = std::max<int64_t>(64, std::min<int64_t>(R, ((int64_t)4 << 30) / per_seq));
+    OCX_HIP(cx->out.ensure((size_t)chunk * 16));
+    for (int64_t r0 = 0; r0 < R; r0 += chunk) {
+        const int64_t nb = std::min(chunk, R - r0);
+        ocx_layout L;
+        if (int rc = ocx_layout_init(nb, T, d, -1, &L)) return rc;
+        OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
+        OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
+        OCX_HIP(ocx_launch_gen_gT_raw(&L, base_seed, run0 + r0, cx->zt.as<double>(),
+                                      cx->yt.as<double>(), st));
+        float* res = reinterpret_cast<float*>(cx->out.as<double>() + chunk);
+        OCX_HIP(ocx_launch_twin32(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr, 1,
+                                  res, nullptr, nullptr, nullptr, st));
+        OCX_HIP(hipMemcpyAsync(regrets + r0, res, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+        OCX_HIP(hipStreamSynchronize(st));
+    }
+    return OCX_OK;
+}
+
 }  // extern "C"

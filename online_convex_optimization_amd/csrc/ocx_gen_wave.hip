@@ -449,7 +449,9 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 // LR (DF = 64 only): the low-LDS form for few-stream batches: 7 rows per epilogue batch
 // (7·64 + 63 pending normals fit 512 doubles) so the ring is 4 KB per wave and six waves
 // per SIMD fit the LDS; the default form's 8-row batches need 1024 (4 waves per SIMD).
-template <int MODE, int DF, bool LR = false>
+// RAW (DF = 0 only): rows left unclipped, for the float32 twin (ocx_twin32.hip), which
+// rounds them to float and clips them in float32 itself (algorithms.py:157-160).
+template <int MODE, int DF, bool LR = false, bool RAW = false>
 __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
@@ -622,7 +624,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
 #ifdef OCX_GEN_TUNE_NO_NORM  // tuning only: no row norms (unclipped rows)
                 if (false) {
 #else
-                if (d <= 128) {
+                if (!RAW && d <= 128) {
 #endif
                     const int r = d < 8 ? lane : (lane >> 3);
                     const unsigned o = tailp + (unsigned)(r * d);
@@ -686,7 +688,9 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
                     for (int r = 0; r < nrows; ++r) {
                         const unsigned o = tailp + (unsigned)(r * d);
                         double scr;
-                        if (d > 128) {
+                        if (RAW) {
+                            scr = 1.0;
+                        } else if (d > 128) {
                             const double nrm = sqrt(row_sumsq(ring, rmask, o, d, lane, stk));
                             scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
                         } else {
@@ -757,7 +761,7 @@ int ring_doubles(int64_t d, int DF, bool LR = false) {
     return rb;
 }
 
-template <int MODE, int DF, bool LR = false>
+template <int MODE, int DF, bool LR = false, bool RAW = false>
 hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
                           int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
                           double* ytl, const uint64_t* st_in, uint64_t* st_out,
@@ -776,7 +780,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
         const int n = std::atoi(ev);
         if (n > 0 && n < cus) cus = n;
     }
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF, LR>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF, LR, RAW>,
                                                      kWaveBlock, lds);
     if (e != hipSuccess) return e;
     int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
@@ -790,7 +794,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
     const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));
-    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR>), dim3(blocks), dim3(kWaveBlock), lds, st,
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR, RAW>), dim3(blocks), dim3(kWaveBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
                        st_out, lab_in, lab_out, rb, nwaves);
     return hipGetLastError();
@@ -848,6 +852,16 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
     if (nseq == 0 || L->T == 0) return hipSuccess;
     return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt,
                           ytl, nullptr, nullptr, nullptr, nullptr, st);
+}
+
+hipError_t ocx_launch_gen_gT_raw(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
+                                 double* ytl, hipStream_t st) {
+    const int64_t nseq = L->G * L->S;
+    if (nseq == 0 || L->T == 0) return hipSuccess;
+    if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    return launch_wave_df<0, 0, false, true>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P,
+                                             L->C, L->G, zt, ytl, nullptr, nullptr, nullptr,
+                                             nullptr, st);
 }
 
 hipError_t ocx_launch_gen_seek(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,

@@ -30,6 +30,9 @@ hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st);
+// the g(T) sampler's normals unclipped (the float32 twin clips them itself)
+hipError_t ocx_launch_gen_gT_raw(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
+                                 double* ytl, hipStream_t st);
 hipError_t ocx_launch_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
                                  const uint64_t* stream_ids, double p, int64_t block_len,
                                  double* zt, double* ytl, hipStream_t st);
@@ -48,3 +51,11 @@ hipError_t ocx_launch_ftrl_exact(const ocx_layout* L, const double* zt, const do
                                  double eta0, double* cum_r, double* cum_e, double* comp_e,
                                  double* comp_f, double* cmp_out, int* regime, hipStream_t st,
                                  int onepass = 0, int norm = 0);
+// float32 twin (algorithms.py, ocx_twin32.hip): P = 1 layouts, d <= 32
+// algo 0 FTRL, 1 FTL, 2 SMART (thresh[B]); clip: rows are raw g(T) normals to round to
+// float and clip in float32 (algorithms.py:157-160)
+hipError_t ocx_launch_twin32(const ocx_layout* L, const double* zt, const double* yt, int algo,
+                             double eta0, const double* thresh, int clip, float* result,
+                             double* cum, float* comp, int64_t* sw, hipStream_t st);
+hipError_t ocx_launch_pack32(const ocx_layout* L, const float* z, const float* y, double* zt,
+                             double* ytl, hipStream_t st);

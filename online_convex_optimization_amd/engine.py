@@ -212,6 +212,53 @@ def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float
     return out
 
 
+TWIN32_ALGOS = {"FTRL": 0, "FTL": 1, "SMART": 2}
+
+
+def twin32_batch(z, y, algo: int = 0, eta0: float = SQRT2, thresh=None, *, device: int = 0,
+                 return_all: bool = False):
+    """The float32 twin (algorithms.py:28-54 simulate_alg, algo 0 FTRL / 1 FTL; :65-120
+    simulate_SMART_like, algo 2 with thresh scalar or [B]) over B sequences, in NumPy 2's
+    float32 arithmetic; d <= 32.
+
+    z [B, T, d] and y [B, T] are taken as float32 (the twin's callers pass float32).
+    Returns the twin's np.float32 results [B] or, with ``return_all``, (result, cum_loss
+    float64, comp_loss float32, switch_step int64; -1 = no switch / not SMART)."""
+    z = np.ascontiguousarray(z, dtype=np.float32)
+    y = np.ascontiguousarray(y, dtype=np.float32)
+    B, T, d = _check_zy(z, y)
+    algo = int(algo)
+    if algo not in (0, 1, 2):
+        raise ValueError("algo must be 0 (FTRL), 1 (FTL) or 2 (SMART)")
+    th = None
+    if algo == 2:
+        if thresh is None:
+            raise ValueError("SMART needs thresh")
+        th = _f64(np.broadcast_to(np.asarray(thresh, dtype=np.float64), (B,)))
+    res = np.zeros(B, dtype=np.float32)
+    cum = np.zeros(B) if return_all else None
+    comp = np.zeros(B, dtype=np.float32) if return_all else None
+    sw = np.full(B, -1, dtype=np.int64) if return_all else None
+    fp = _lib.c_fp
+    _lib.call("ocx_twin32_batch", z.ctypes.data_as(fp), y.ctypes.data_as(fp), B, T, d, algo,
+              float(eta0), ptr(th), res.ctypes.data_as(fp), ptr(cum),
+              comp.ctypes.data_as(fp) if comp is not None else None,
+              sw.ctypes.data_as(_lib.c_i64p) if sw is not None else None, int(device))
+    return (res, cum, comp, sw) if return_all else res
+
+
+def twin32_gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5,
+                      eta0: float = SQRT2, run0: int = 0, device: int = 0) -> np.ndarray:
+    """The float32 twin's g(T) regrets (algorithms.py:150-169) for runs [run0, run0+runs),
+    generated and simulated on device: float32 [runs]."""
+    if base_seed < 0 or base_seed >= 2 ** 64:
+        raise ValueError("base_seed must be in [0, 2**64)")
+    out = np.zeros(int(runs), dtype=np.float32)
+    _lib.call("ocx_twin32_gT_regrets", int(base_seed), int(T), int(run0), int(runs), int(d),
+              float(eta0), out.ctypes.data_as(_lib.c_fp), int(device))
+    return out
+
+
 def release_buffers(device: int = 0) -> None:
     """Free the HBM the engine caches on `device` for host-array calls and g(T) sweeps
     (it regrows on the next call): do this before allocating a large DeviceBatch."""

@@ -362,3 +362,187 @@ def noisy_iid_sample(run_seed: int, T: int, rep: int = 0, p: float = 0.10, d: in
     flips = gen.random(T) < p
     y[flips] *= -1.0
     return z, y, u
+
+
+# ---------------------------------------------------------------------------
+# float32 twin (algorithms.py:10-171) in explicit operation order
+# ---------------------------------------------------------------------------
+# The twin's NumPy calls, as this image's NumPy 2.2 / OpenBLAS 0.3.29 compute them
+# (probed, and pinned by tests/golden/twin32.npz, made by running the calls themselves):
+#   sdot (np.dot, np.linalg.norm, 1-D @ 1-D), n < 32: float products summed in double;
+#   sgemv (z @ x): rows in blocks of four by a float fma chain over the columns, the
+#     n mod 4 tail rows by a plain float chain, a one-row matrix by the sdot rule (d = 5);
+#   np.sum (float32): pairwise (leaves <= 128, 8 accumulators) per 8192-element buffer;
+#   NEP 50: Python scalars take float32; Python float - np.float32 -> float32.
+# Only the fma is emulated through float64 (exact product, then the sum rounded twice):
+# the double rounding differs from a true fma with probability ~2^-29 per operation.
+
+_F = np.float32
+
+
+def t32_sdot(a, b) -> np.float32:
+    """OpenBLAS sdot for n < 32 (algorithms.py:14, :19, :41, :91)."""
+    p = (np.asarray(a, _F) * np.asarray(b, _F)).astype(np.float64)
+    acc = 0.0
+    for v in p:
+        acc += float(v)
+    return _F(acc)
+
+
+def t32_gemv(z, x) -> np.ndarray:
+    """z @ x for a float32 [n, d] matrix (algorithms.py:52, :110, :117)."""
+    z = np.asarray(z, _F)
+    x = np.asarray(x, _F)
+    n, d = z.shape
+    if n == 1:
+        return np.array([t32_sdot(z[0], x)], dtype=_F)
+    nb = 4 * (n // 4)
+    q = np.empty(n, dtype=_F)
+    acc = np.zeros(nb, dtype=_F)
+    for j in range(d):
+        acc = (z[:nb, j].astype(np.float64) * float(x[j]) + acc.astype(np.float64)).astype(_F)
+    q[:nb] = acc
+    acc = np.zeros(n - nb, dtype=_F)
+    for j in range(d):
+        acc = acc + z[nb:, j] * x[j]
+    q[nb:] = acc
+    return q
+
+
+def _t32_leaf(a: np.ndarray) -> np.float32:
+    n = len(a)
+    if n < 8:
+        r = _F(-0.0)
+        for v in a:
+            r = _F(r + v)
+        return r
+    m = n - n % 8
+    r = a[:8].copy()
+    for i in range(8, m, 8):
+        r = r + a[i:i + 8]
+    res = _F(_F(_F(r[0] + r[1]) + _F(r[2] + r[3])) + _F(_F(r[4] + r[5]) + _F(r[6] + r[7])))
+    for v in a[m:]:
+        res = _F(res + v)
+    return res
+
+
+def _t32_pairwise(a: np.ndarray) -> np.float32:
+    n = len(a)
+    if n <= 128:
+        return _t32_leaf(a)
+    n2 = n // 2
+    n2 -= n2 % 8
+    return _F(_t32_pairwise(a[:n2]) + _t32_pairwise(a[n2:]))
+
+
+def t32_sum(a) -> np.float32:
+    """np.sum of a contiguous float32 vector."""
+    a = np.asarray(a, _F)
+    tot = None
+    for s in range(0, len(a), 8192):
+        p = _t32_pairwise(a[s:s + 8192])
+        tot = p if tot is None else _F(tot + p)
+    return _F(0.0) if tot is None else tot
+
+
+def t32_row_norms(z) -> np.ndarray:
+    """np.linalg.norm(z, axis=1) of a float32 [n, d] matrix (algorithms.py:159)."""
+    z = np.asarray(z, _F)
+    sq = z * z
+    return np.sqrt(np.array([_t32_leaf(r) for r in sq], dtype=_F))
+
+
+def t32_action_ftl(theta) -> np.ndarray:
+    """algorithms.py:13-15."""
+    n = np.sqrt(t32_sdot(theta, theta))
+    if n == 0.0:
+        return np.zeros_like(theta)
+    return (-(_F(1.0) / n)) * theta
+
+
+def t32_action_ftrl(theta, t: int, eta0: float) -> np.ndarray:
+    """algorithms.py:17-21."""
+    x = _F(-(eta0 / math.sqrt(max(1, t)))) * theta
+    n = np.sqrt(t32_sdot(x, x))
+    if n > 1.0:
+        x = x * (_F(1.0) / n)
+    return x
+
+
+def _t32_grad(diff: float) -> float:
+    return 0.5 if diff > 0.0 else -0.5 if diff < 0.0 else 0.0
+
+
+def _t32_comp(z, y, x) -> np.float32:
+    return t32_sum(_F(0.5) * np.abs(t32_gemv(z, x) - y))
+
+
+def t32_simulate_alg_full(z, y, alg_flag: int, eta0: float):
+    """algorithms.py:28-54 → (np.float32 result, cum_loss, comp_loss)."""
+    z = np.ascontiguousarray(z, dtype=_F)
+    y = np.ascontiguousarray(y, dtype=_F)
+    T, d = z.shape
+    theta = np.zeros(d, dtype=_F)
+    cum = 0.0
+    for t in range(T):
+        x = t32_action_ftrl(theta, t + 1, eta0) if alg_flag == 0 else t32_action_ftl(theta)
+        q = float(t32_sdot(z[t], x))
+        yt = float(y[t])
+        cum += 0.5 * abs(q - yt)
+        theta = theta + _F(_t32_grad(q - yt)) * z[t]
+    comp = _t32_comp(z, y, t32_action_ftl(theta))
+    return _F(_F(cum) - comp), cum, comp
+
+
+def t32_simulate_smart_full(z, y, theta_thresh: float, eta0: float):
+    """algorithms.py:65-120 → (np.float32 result, total_loss, comp_loss, switch step or -1)."""
+    z = np.ascontiguousarray(z, dtype=_F)
+    y = np.ascontiguousarray(y, dtype=_F)
+    T, d = z.shape
+    th_ftl = np.zeros(d, dtype=_F)
+    th_ftrl = np.zeros(d, dtype=_F)
+    thr = _F(theta_thresh)
+    switched, sw = False, -1
+    ftl_loss = total = 0.0
+    for t in range(T):
+        yt = float(y[t])
+        pf = float(t32_sdot(z[t], t32_action_ftl(th_ftl)))
+        th_ftl = th_ftl + _F(_t32_grad(pf - yt)) * z[t]
+        lf = 0.5 * abs(pf - yt)
+        ftl_loss += lf
+        if switched:
+            pr = float(t32_sdot(z[t], t32_action_ftrl(th_ftrl, t + 1, eta0)))
+            total += 0.5 * abs(pr - yt)
+            th_ftrl = th_ftrl + _F(_t32_grad(pr - yt)) * z[t]
+        else:
+            total += lf
+            sl = _t32_comp(z[:t + 1], y[:t + 1], t32_action_ftl(th_ftl))
+            if _F(_F(ftl_loss) - sl) >= thr:
+                switched, sw = True, t
+    comp = _t32_comp(z, y, t32_action_ftl(th_ftl))
+    return _F(_F(total) - comp), total, comp, sw
+
+
+def t32_gT_sample(base_seed: int, T: int, run: int, d: int = 5):
+    """The twin's g(T) sampler (algorithms.py:155-163) with ``d`` as a parameter."""
+    gen = rng(base_seed, T, run)
+    z = gen.standard_normal((T, d)).astype(_F)
+    norms = t32_row_norms(z)[:, None]
+    z = z * (_F(1.0) / np.maximum(norms, _F(1.0)))
+    y = gen.choice([-1.0, 1.0], size=T).astype(_F)
+    return z, y
+
+
+def t32_empirical_worst_case_thresholds(T_grid, *, runs: int = 5, base_seed: int = 0):
+    """algorithms.py:135-171."""
+    out = {}
+    for T_val in T_grid:
+        T = int(T_val)
+        m = 0.0
+        for r in range(runs):
+            z, y = t32_gT_sample(base_seed, T, r)
+            reg = t32_simulate_alg_full(z, y, 0, math.sqrt(2))[0]
+            if reg > m:
+                m = reg
+        out[T] = m
+    return out
