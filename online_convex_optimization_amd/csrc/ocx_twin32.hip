@@ -18,6 +18,7 @@
 // T <= 1000, d = 5) and its SMART re-reads the whole prefix every step (:109-111); rows
 // are read in blocks of up to 8 steps so their loads are in flight together.
 #include <algorithm>
+#include <cstdlib>
 
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
@@ -35,86 +36,6 @@ __device__ __forceinline__ float t32_div(float a, float b) { return (float)((dou
 __device__ __forceinline__ float t32_tree8(const float (&r)[8]) {
     return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
 }
-
-// np.sum of a float32 vector whose elements arrive one at a time (every lane of the wave
-// sums a vector of the same length, so the recursion is uniform).  The recursion
-// pw(n) = n <= 128 ? leaf(n) : pw(n2) + pw(n - n2), n2 = n/2 rounded down to a multiple of
-// 8, is walked in post order: a frame per pending right half, holding the left half's sum.
-struct Pw32 {
-    int64_t left;  // elements still to come
-    float total;
-    bool any;
-    int sp, ln, li;  // frames in use; current leaf's length and position
-    int fr_len[8];
-    float fr_val[8];
-    bool fr_has[8];
-    float r[8];
-    float res;
-
-    __device__ void begin(int64_t n) {
-        left = n;
-        total = 0.0f;
-        any = false;
-        if (n > 0) buffer();
-    }
-    __device__ void buffer() {
-        sp = 0;
-        descend(left < kPwBuf ? (int)left : kPwBuf);
-    }
-    __device__ void descend(int n) {
-        while (n > kPwBlock) {
-            int n2 = n / 2;
-            n2 -= n2 % 8;
-            fr_len[sp] = n - n2;
-            fr_has[sp] = false;
-            ++sp;
-            n = n2;
-        }
-        ln = n;
-        li = 0;
-        res = -0.0f;
-    }
-    __device__ void push(float v) {
-        if (ln < 8) {
-            res = res + v;
-        } else {
-            const int m = ln - (ln & 7);
-            if (li < m) {
-                const int k = li & 7;
-                const bool first = li < 8;
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    if (q == k) r[q] = first ? v : r[q] + v;
-            } else {
-                if (li == m) res = t32_tree8(r);
-                res = res + v;
-            }
-        }
-        ++li;
-        --left;
-        if (li == ln) done((ln >= 8 && (ln & 7) == 0) ? t32_tree8(r) : res);
-    }
-    __device__ void done(float v) {
-        for (;;) {
-            if (sp == 0) {  // a buffer's sum
-                total = any ? total + v : v;
-                any = true;
-                if (left > 0) buffer();
-                return;
-            }
-            const int top = sp - 1;
-            if (!fr_has[top]) {  // left half done: walk the right half
-                fr_val[top] = v;
-                fr_has[top] = true;
-                descend(fr_len[top]);
-                return;
-            }
-            v = fr_val[top] + v;
-            --sp;
-        }
-    }
-    __device__ float value() const { return any ? total : 0.0f; }
-};
 
 // sdot, n < 32: float products summed in double (padding coordinates add +0)
 template <int C>
@@ -236,24 +157,95 @@ __device__ __forceinline__ void t32_rows(const T32Seq& q, int64_t t0, int64_t n,
         }
 }
 
-// np.sum(0.5 * np.abs(z[:n] @ x - y[:n])) (algorithms.py:52-53, :110-111, :117-118)
+// 0.5 * |row i of z @ x - y_i| in float32, rows [s, s + NB) below e
+template <int C, int NB>
+__device__ __forceinline__ void t32_block_losses(const T32Seq& q, const float (&x)[C], int64_t n,
+                                                 int64_t s, int64_t e, float (&l)[NB]) {
+    float zb[NB][C], yb[NB];
+    t32_rows<C, NB>(q, s, e, zb, yb);
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+        l[u] = s + u < e ? 0.5f * fabsf(t32_gemv_row<C>(zb[u], x, s + u, n) - yb[u]) : 0.0f;
+}
+
+// One leaf of NumPy's pairwise sum: m losses from row s (every leaf of a buffer longer
+// than 7 starts at a multiple of 8, since the recursion cuts at multiples of 8): eight
+// accumulators over the whole groups of 8, their tree, then the tail one by one
+template <int C>
+__device__ __forceinline__ float t32_leaf(const T32Seq& q, const float (&x)[C], int64_t n,
+                                          int64_t s, int m) {
+    float l[8];
+    if (m < 8) {
+        t32_block_losses<C, 8>(q, x, n, s, s + m, l);
+        float res = -0.0f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (u < m) res = res + l[u];
+        return res;
+    }
+    const int mfull = m - (m & 7);
+    float r[8];
+    t32_block_losses<C, 8>(q, x, n, s, s + 8, r);
+    for (int i = 8; i < mfull; i += 8) {
+        t32_block_losses<C, 8>(q, x, n, s + i, s + i + 8, l);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = r[u] + l[u];
+    }
+    float res = t32_tree8(r);
+    if (m & 7) {
+        t32_block_losses<C, 8>(q, x, n, s + mfull, s + m, l);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (u < (m & 7)) res = res + l[u];
+    }
+    return res;
+}
+
+// NumPy's pairwise sum of one buffer of nb <= 8192 losses from row s0: pw(m) = m <= 128 ?
+// leaf(m) : pw(m2) + pw(m - m2), m2 = m/2 cut down to a multiple of 8, walked in post
+// order with a frame per pending right half (the frames are touched once per leaf)
+template <int C>
+__device__ float t32_pw_buffer(const T32Seq& q, const float (&x)[C], int64_t n, int64_t s0,
+                               int nb) {
+    int fr_len[8];
+    float fr_val[8];
+    bool fr_has[8];
+    int sp = 0, m = nb;
+    int64_t pos = s0;
+    for (;;) {
+        while (m > kPwBlock) {
+            int m2 = m / 2;
+            m2 -= m2 % 8;
+            fr_len[sp] = m - m2;
+            fr_has[sp] = false;
+            ++sp;
+            m = m2;
+        }
+        float v = t32_leaf<C>(q, x, n, pos, m);
+        pos += m;
+        while (sp > 0 && fr_has[sp - 1]) {
+            v = fr_val[sp - 1] + v;
+            --sp;
+        }
+        if (sp == 0) return v;
+        fr_val[sp - 1] = v;
+        fr_has[sp - 1] = true;
+        m = fr_len[sp - 1];
+    }
+}
+
+// np.sum(0.5 * np.abs(z[:n] @ x - y[:n])) (algorithms.py:52-53, :110-111, :117-118):
+// one pairwise sum per 8192-element buffer, the buffers added in order
 template <int C>
 __device__ __attribute__((noinline)) float t32_loss_sum(const T32Seq& q, const float (&x)[C],
                                                         int64_t n) {
-    constexpr int NB = t32_nb(C);
-    Pw32 pw;
-    pw.begin(n);
-    for (int64_t i0 = 0; i0 < n; i0 += NB) {
-        float zb[NB][C], yb[NB];
-        t32_rows<C, NB>(q, i0, n, zb, yb);
-#pragma unroll
-        for (int u = 0; u < NB; ++u)
-            if (i0 + u < n) {
-                const float qv = t32_gemv_row<C>(zb[u], x, i0 + u, n);
-                pw.push(0.5f * fabsf(qv - yb[u]));
-            }
+    float total = 0.0f;
+    for (int64_t s0 = 0; s0 < n; s0 += kPwBuf) {
+        const int nb = (int)(n - s0 < kPwBuf ? n - s0 : kPwBuf);
+        const float p = t32_pw_buffer<C>(q, x, n, s0, nb);
+        total = s0 == 0 ? p : total + p;
     }
-    return pw.value();
+    return total;
 }
 
 template <int C>
@@ -349,10 +341,220 @@ __global__ __launch_bounds__(64) void ocx_twin32_kernel(
     }
 }
 
+// ---- SMART, one wavefront per sequence --------------------------------------------------
+// simulate_SMART_like re-sums its whole prefix every step before the switch (:109-111):
+// O(T^2) work per sequence, latency-bound in a lane of its own (T = 1000: 0.3 s for one
+// sequence, against ~20 ms for NumPy).  Here the sequence's rows sit in LDS as float and
+// the wave splits each prefix sum the way NumPy's pairwise recursion does: its leaves (of
+// <= 128 losses, all starting at multiples of 8) and their eight accumulator chains are
+// independent, so lane 8*i + k runs chain k of leaf i; lane 8*i then folds the chains
+// (tree of 8) and the leaf's tail, and the leaf sums are combined in the recursion's post
+// order.  The scalar part of the step (actions, theta updates) runs on every lane alike.
+constexpr int kWaveLeaves = 128;  // leaves of an 8192-element buffer: at most 8192/64
+
+struct T32Wave {
+    const float* z;  // LDS rows [T][C]
+    const float* y;  // LDS labels [T]
+    float* red;      // [64]
+    int* lstart;     // [kWaveLeaves]
+    int* llen;
+    float* lsum;
+};
+
+template <int C>
+__device__ __forceinline__ float t32_wave_loss(const T32Wave& w, const float (&x)[C], int i, int n) {
+    float zr[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) zr[j] = w.z[i * C + j];
+    return 0.5f * fabsf(t32_gemv_row<C>(zr, x, i, n) - w.y[i]);
+}
+
+// np.sum(0.5 * np.abs(z[:n] @ x - y[:n])), n <= 8192 (one NumPy buffer), on the whole wave
+template <int C>
+__device__ float t32_wave_loss_sum(const T32Wave& w, const float (&x)[C], int n, int lane) {
+    if (n == 0) return 0.0f;
+    // the leaves, in order
+    int nl = 0;
+    {
+        int stk[8];
+        int sp = 0, m = n, pos = 0;
+        for (;;) {
+            while (m > kPwBlock) {
+                int m2 = m / 2;
+                m2 -= m2 % 8;
+                stk[sp++] = m - m2;
+                m = m2;
+            }
+            if (lane == 0) {
+                w.lstart[nl] = pos;
+                w.llen[nl] = m;
+            }
+            ++nl;
+            pos += m;
+            if (sp == 0) break;
+            m = stk[--sp];
+        }
+    }
+    __syncthreads();
+    for (int base = 0; base < nl; base += 8) {
+        const int leaf = base + (lane >> 3), k = lane & 7;
+        int s = 0, m = 0;
+        if (leaf < nl) {
+            s = w.lstart[leaf];
+            m = w.llen[leaf];
+        }
+        const int mfull = m - (m & 7);
+        float r = 0.0f;
+        if (m >= 8) {
+            r = t32_wave_loss<C>(w, x, s + k, n);
+            for (int i = s + k + 8; i < s + mfull; i += 8) r = r + t32_wave_loss<C>(w, x, i, n);
+        }
+        w.red[lane] = r;
+        __syncthreads();
+        if (k == 0 && leaf < nl) {
+            float res;
+            int i0;
+            if (m >= 8) {
+                float rr[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) rr[u] = w.red[lane + u];
+                res = t32_tree8(rr);
+                i0 = s + mfull;
+            } else {
+                res = -0.0f;
+                i0 = s;
+            }
+            for (int i = i0; i < s + m; ++i) res = res + t32_wave_loss<C>(w, x, i, n);
+            w.lsum[leaf] = res;
+        }
+        __syncthreads();
+    }
+    // the recursion's post order over the leaf sums
+    int fr_len[8];
+    float fr_val[8];
+    bool fr_has[8];
+    int sp = 0, m = n, li = 0;
+    for (;;) {
+        while (m > kPwBlock) {
+            int m2 = m / 2;
+            m2 -= m2 % 8;
+            fr_len[sp] = m - m2;
+            fr_has[sp] = false;
+            ++sp;
+            m = m2;
+        }
+        float v = w.lsum[li++];
+        while (sp > 0 && fr_has[sp - 1]) {
+            v = fr_val[sp - 1] + v;
+            --sp;
+        }
+        if (sp == 0) {
+            __syncthreads();  // leaf arrays are rewritten by the next call
+            return v;
+        }
+        fr_val[sp - 1] = v;
+        fr_has[sp - 1] = true;
+        m = fr_len[sp - 1];
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(64) void ocx_twin32_smart_wave_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t G, double eta0, const double* __restrict__ thresh, float* __restrict__ result,
+    double* __restrict__ cum_out, float* __restrict__ comp_out, int64_t* __restrict__ sw_out) {
+    extern __shared__ float t32_lds[];
+    __shared__ float red[64];
+    __shared__ int lstart[kWaveLeaves], llen[kWaveLeaves];
+    __shared__ float lsum[kWaveLeaves];
+    const int lane = threadIdx.x;
+    const int64_t b = blockIdx.x;
+    const int n = (int)T;
+    float* zs = t32_lds;
+    float* ys = t32_lds + (int64_t)n * C;
+    {
+        // stage the sequence (lane L of wave-group g in the P = 1 layout) as float rows
+        const int64_t g = b / 64;
+        const int sl = (int)(b % 64);
+        const ocx_d2* zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * 64 + sl;
+        const int64_t kst = G * T * 64;
+        for (int t = lane; t < n; t += 64) {
+#pragma unroll
+            for (int k = 0; k < C / 2; ++k) {
+                const ocx_d2 v = zp[(int64_t)t * 64 + k * kst];
+                zs[t * C + 2 * k] = (float)v.x;
+                zs[t * C + 2 * k + 1] = (float)v.y;
+            }
+            ys[t] = (float)yt[(g * T + t) * 64 + sl];
+        }
+    }
+    __syncthreads();
+    T32Wave w{zs, ys, red, lstart, llen, lsum};
+    float th[C], thr[C], x[C], sx[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = thr[j] = 0.0f;
+    const float th32 = (float)thresh[b];
+    bool switched = false;
+    double ftl_loss = 0.0, cum = 0.0;
+    int64_t sw = -1;
+    for (int t = 0; t < n; ++t) {
+        float zr[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) zr[j] = zs[t * C + j];
+        const double yv = (double)ys[t];
+        t32_ftl<C>(th, x);
+        const double pf = (double)t32_sdot<C>(zr, x);
+        const float gf = (float)t32_grad(pf - yv);
+#pragma unroll
+        for (int j = 0; j < C; ++j) th[j] = th[j] + gf * zr[j];
+        const double lf = 0.5 * fabs(pf - yv);
+        ftl_loss += lf;
+        if (switched) {
+            t32_ftrl<C>(thr, t + 1, eta0, x);
+            const double pr = (double)t32_sdot<C>(zr, x);
+            cum += 0.5 * fabs(pr - yv);
+            const float gr = (float)t32_grad(pr - yv);
+#pragma unroll
+            for (int j = 0; j < C; ++j) thr[j] = thr[j] + gr * zr[j];
+        } else {
+            cum += lf;
+            t32_ftl<C>(th, sx);
+            const float sl = t32_wave_loss_sum<C>(w, sx, t + 1, lane);
+            if ((float)ftl_loss - sl >= th32) {
+                switched = true;
+                sw = t;
+            }
+        }
+    }
+    t32_ftl<C>(th, x);
+    const float comp = t32_wave_loss_sum<C>(w, x, n, lane);
+    if (lane == 0) {
+        result[b] = (float)cum - comp;
+        if (cum_out) cum_out[b] = cum;
+        if (comp_out) comp_out[b] = comp;
+        if (sw_out) sw_out[b] = sw;
+    }
+}
+
+constexpr int64_t kWaveLdsBytes = 60 * 1024;  // rows of one sequence staged in LDS (<= 64 KB with the static arrays)
+
 template <int C>
 hipError_t launch_t32(const ocx_layout* L, const double* zt, const double* yt, int algo,
                       double eta0, const double* thresh, int clip, float* result, double* cum,
                       float* comp, int64_t* sw, hipStream_t st) {
+    const int64_t lds = L->T * (C + 1) * 4;
+    // OCX_TWIN32_SMART_LANES=1 (tests): the lane-per-sequence kernel for SMART as well
+    static const bool lanes_only = [] {
+        const char* e = std::getenv("OCX_TWIN32_SMART_LANES");
+        return e != nullptr && e[0] == '1';
+    }();
+    if (algo == 2 && !clip && lds <= kWaveLdsBytes && !lanes_only) {
+        // SMART: a wavefront per sequence wherever the rows fit the LDS (T <= 2340 at d = 5)
+        hipLaunchKernelGGL((ocx_twin32_smart_wave_kernel<C>), dim3((unsigned)L->B), dim3(64),
+                           (size_t)lds, st, zt, yt, L->B, L->T, L->G, eta0, thresh, result, cum,
+                           comp, sw);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((ocx_twin32_kernel<C>), dim3((unsigned)L->G), dim3(64), 0, st, zt, yt, L->B,
                        L->T, L->G, (int)L->d, algo, eta0, thresh, clip, result, cum, comp, sw);
     return hipGetLastError();

@@ -109,3 +109,37 @@ def test_dropin_module(fx):
     g = A.empirical_worst_case_thresholds(fx["gT_grid"], runs=8)
     assert [g[int(T)] for T in fx["gT_grid"]] == list(fx["gT_grid_g"])
     assert all(type(v) is np.float32 for v in g.values())
+
+
+def test_smart_wave_and_lane_kernels_agree(eng):
+    """SMART runs a wavefront per sequence while its rows fit the LDS and a lane per
+    sequence beyond; both against each other (subprocess: the choice is read once) and
+    the lane kernel past the LDS limit against the oracle."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(77)
+    B, T, d = 5, 400, 5
+    z = (rng.standard_normal((B, T, d)) * 0.5).astype(F)
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0).astype(F)
+    th = np.array([0.5, 3.0, 8.0, 1e9, 12.0])
+    want = eng.twin32_batch(z, y, 2, SQ2, thresh=th, return_all=True)
+    code = ("import sys, numpy as np; from online_convex_optimization_amd import engine; "
+            "a = np.load(sys.argv[1]); r = engine.twin32_batch(a['z'], a['y'], 2, 2 ** 0.5, "
+            "thresh=a['th'], return_all=True); np.savez(sys.argv[2], *r)")
+    import tempfile
+    with tempfile.TemporaryDirectory() as tmp:
+        src, dst = os.path.join(tmp, "in.npz"), os.path.join(tmp, "out.npz")
+        np.savez(src, z=z, y=y, th=th)
+        env = dict(os.environ, OCX_TWIN32_SMART_LANES="1")
+        subprocess.run([sys.executable, "-c", code, src, dst], check=True, env=env, timeout=120,
+                       cwd=os.path.dirname(HERE))
+        with np.load(dst) as got:
+            for i in range(4):
+                assert np.array_equal(got[f"arr_{i}"], want[i]), i
+    # beyond the LDS limit (T * (C + 1) * 4 > 60 KB): the lane kernel, against the oracle
+    T = 2300
+    z = (rng.standard_normal((1, T, d)) * 0.5).astype(F)
+    y = np.where(rng.random((1, T)) < 0.5, -1.0, 1.0).astype(F)
+    r = eng.twin32_batch(z, y, 2, SQ2, thresh=6.0, return_all=True)
+    o = O.t32_simulate_smart_full(z[0], y[0], 6.0, SQ2)
+    assert (r[0][0], r[1][0], r[2][0], r[3][0]) == o
