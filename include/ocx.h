@@ -183,6 +183,11 @@ int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t b
 int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64_t d, int algo,
                      double eta0, const double* thresh, float* result, double* cum_loss,
                      float* comp_loss, int64_t* switch_step, int device);
+/* ocx_twin32_batch on a device-resident batch in a one-lane layout (lanes_per_seq = -1);
+ * thresh (SMART) is a device array [B]; result / comp_loss are float32. */
+int ocx_dev_twin32(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int algo,
+                   double eta0, const double* thresh, float* result, double* cum_loss,
+                   float* comp_loss, int64_t* switch_step, void* stream);
 /* The float32 twin's g(T) inner loop (algorithms.py:150-169): the regrets of runs
  * run0 .. run0+R-1 of _rng(base_seed, T, run), rows rounded to float32 and clipped in
  * float32, FTRL with eta0; on device (generator + twin kernel), nothing but the regrets

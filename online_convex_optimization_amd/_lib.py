@@ -86,6 +86,8 @@ SIGNATURES = {
                                      ctypes.POINTER(c_int), c_int, c_int, c_dp, c_dp]),
     "ocx_twin32_batch": (c_int, [c_fp, c_fp, c_i64, c_i64, c_i64, c_int, c_double, c_dp, c_fp,
                                  c_dp, c_fp, c_i64p, c_int]),
+    "ocx_dev_twin32": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp, c_vp,
+                               c_vp, c_vp, c_vp, c_vp]),
     "ocx_twin32_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_fp, c_int]),
 }
 OCX_ALG_CLIPPED_ROWS = 1

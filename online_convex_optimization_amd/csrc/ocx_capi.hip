@@ -877,6 +877,21 @@ int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64
     return OCX_OK;
 }
 
+int ocx_dev_twin32(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int algo,
+                   double eta0, const double* thresh, float* result, double* cum_loss,
+                   float* comp_loss, int64_t* switch_step, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->P != 1) return fail(OCX_E_INVALID, "the float32 twin needs a one-lane layout (lanes_per_seq = -1)");
+    if (L->d > 32) return fail(OCX_E_UNSUPPORTED, "the float32 twin supports d <= 32");
+    if (algo < 0 || algo > 2) return fail(OCX_E_INVALID, "algo must be 0 (FTRL), 1 (FTL) or 2 (SMART)");
+    if (L->B > 0 && (!result || (algo == 2 && !thresh)))
+        return fail(OCX_E_INVALID, "NULL result / thresh");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    OCX_HIP(ocx_launch_twin32(L, z_tiled, y_tiled, algo, eta0, algo == 2 ? thresh : nullptr, 0,
+                              result, cum_loss, comp_loss, switch_step, (hipStream_t)stream));
+    return OCX_OK;
+}
+
 int ocx_twin32_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
                           double eta0, float* regrets, int device) {
     if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");

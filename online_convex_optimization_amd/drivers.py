@@ -10,7 +10,8 @@ averaging then uses the same NumPy calls as the reference (fast_driver.py:113-12
 the statistics are identical, not merely close.
 
 ``fast_driver_main`` is fast_driver.py:201-220 without the plotting: the g(T) sweep
-(empirical_worst_case_thresholds) followed by the four cases.
+(empirical_worst_case_thresholds) followed by the four cases.  ``driver_main`` is the
+same for driver.py:204-226, which runs the float32 twin (algorithms.py).
 """
 from __future__ import annotations
 
@@ -103,6 +104,72 @@ def fast_driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 10
     stats = {}
     for title in CASE_FAMILIES:
         stats[title] = evaluate_stream_with_stats(
+            title, T_grid, g_emp, runs=runs_by_title.get(title, 1),
+            replicates=replicates_by_title.get(title, 1), base_seed=base_seed, device=device)
+    return g_emp, stats
+
+
+# ---------------------------------------------------------------------------
+# driver.py: the same sweep on the float32 twin (algorithms.py)
+# ---------------------------------------------------------------------------
+
+def case_regrets_twin32(title: str, T: int, g_emp_T: float, *, runs: int, replicates: int,
+                        base_seed: int = 0, d: int = 5, p: float = 0.10, block_len: int = 20,
+                        device: int = 0) -> Dict[str, np.ndarray]:
+    """driver.py:86-111 for every (run, rep) of one case and T at once: the four twin
+    algorithms (algorithms.py) on the device-generated family, float32 regrets
+    [runs, replicates]."""
+    family, stream0 = CASE_FAMILIES[title]
+    B = runs * replicates
+    db = engine.DeviceBatch(B, T, d, lanes_per_seq=-1, device=device)  # one lane per sequence
+    run_idx = np.repeat(np.arange(runs), replicates)
+    rep_idx = np.tile(np.arange(replicates), runs)
+    db.generate_family(family, base_seed + 2025 * (run_idx + 1), stream0 + rep_idx, p=p,
+                       block_len=block_len)
+    out = {"FTRL": db.simulate_twin32(0, SQRT2), "FTL": db.simulate_twin32(1, SQRT2),
+           "SMART": db.simulate_twin32(2, SQRT2, math.sqrt(2 * T)),
+           "EMP": db.simulate_twin32(2, SQRT2, float(g_emp_T))}  # driver.py:95 float(g_emp[T])
+    return {k: v[:B].cpu().numpy().reshape(runs, replicates) for k, v in out.items()}
+
+
+def driver_evaluate_stream_with_stats(title: str, T_grid: Sequence[int],
+                                      g_emp: Mapping[int, float], *, runs: int = 1,
+                                      replicates: int = 1, base_seed: int = 0,
+                                      device: int = 0) -> Stats:
+    """driver.py:70-136 for the CASES entry ``title`` (float32 twin): mean regret and 95 % CI
+    per T, the replicate means taken over the twin's np.float32 values as driver.py does."""
+    by_T = {k: [[] for _ in range(len(T_grid))] for k in ALGO_KEYS}
+    per_T = [case_regrets_twin32(title, int(T), g_emp[int(T)], runs=runs, replicates=replicates,
+                                 base_seed=base_seed, device=device) for T in T_grid]
+    for run in range(runs):
+        for ti in range(len(T_grid)):
+            for k in ALGO_KEYS:
+                by_T[k][ti].append(float(np.mean(list(per_T[ti][k][run]))))
+    stats: Stats = {}
+    for k in ALGO_KEYS:
+        means, cis = [], []
+        for vals in by_T[k]:
+            arr = np.asarray(vals, dtype=float)
+            means.append(float(np.mean(arr)) if arr.size else 0.0)
+            cis.append(CI_Z * _sem(arr) if arr.size > 1 else 0.0)
+        stats[k] = (np.array(means, dtype=float), np.array(cis, dtype=float))
+    return stats
+
+
+def driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 1000,
+                base_seed: int = 0, runs_by_title: Optional[Mapping[str, int]] = None,
+                replicates_by_title: Optional[Mapping[str, int]] = None,
+                device: int = 0):
+    """driver.py:204-226 minus the figures (float32 twin): (g_emp, stats_by_case)."""
+    from . import algorithms
+    T_grid = list(range(100, 1100, 100)) if T_grid is None else [int(t) for t in T_grid]
+    runs_by_title = RUNS_BY_TITLE if runs_by_title is None else runs_by_title
+    replicates_by_title = REPLICATES_BY_TITLE if replicates_by_title is None else replicates_by_title
+    g_emp = algorithms.empirical_worst_case_thresholds(np.asarray(T_grid), runs=g_runs,
+                                                       base_seed=base_seed)
+    stats = {}
+    for title in CASE_FAMILIES:
+        stats[title] = driver_evaluate_stream_with_stats(
             title, T_grid, g_emp, runs=runs_by_title.get(title, 1),
             replicates=replicates_by_title.get(title, 1), base_seed=base_seed, device=device)
     return g_emp, stats

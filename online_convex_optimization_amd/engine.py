@@ -430,6 +430,23 @@ class DeviceBatch:
         self._keep_th = self._hold(th)
         return self.regret
 
+    def simulate_twin32(self, algo: int = 0, eta0: float = SQRT2, thresh=None):
+        """The float32 twin (algorithms.py; twin32_batch) on the resident batch, which must
+        use the one-lane layout (``lanes_per_seq=-1``): float32 results [B] on device."""
+        torch = self.torch
+        th = None
+        with self._on_stream():
+            res = torch.empty(max(self.L.B, 1), dtype=torch.float32, device=self.device)
+            if int(algo) == 2:
+                th = torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
+                                                     (self.L.B,)).copy()).to(self.device)
+        _lib.call("ocx_dev_twin32", self._lp(), self.z.data_ptr(), self.y.data_ptr(), int(algo),
+                  float(eta0), th.data_ptr() if th is not None else None, res.data_ptr(), None,
+                  None, None, self._sp)
+        if th is not None:
+            self._keep_th = self._hold(th)
+        return res
+
     def ftl_exact(self, cmp_action=None, regime=None, norm: str = "l2"):
         """Exact FTL (l2 ball, closed form; see ftl_exact_batch) on the resident batch:
         self.cum / self.comp get the replay and comparator losses, ``cmp_action``

@@ -39,6 +39,9 @@ def main():
                         "s": timed(lambda: engine.twin32_batch(zb, yb, 0, math.sqrt(2)), 3)})
             out.append({"what": f"twin32_batch SMART B={B} T={T} (no switch)",
                         "s": timed(lambda: engine.twin32_batch(zb, yb, 2, math.sqrt(2), thresh=1e9), 1)})
+    from online_convex_optimization_amd import drivers
+    s = timed(lambda: drivers.driver_main(), reps=1)
+    out.append({"what": "drivers.driver_main() (driver.py:204-226 without figures, defaults)", "s": s})
     for r in out:
         print(json.dumps(r), flush=True)
 
