@@ -173,6 +173,13 @@ int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t b
                          int64_t d, double eta0, const int* devices, int ndev, int lanes_per_seq,
                          double* gmax, double* regrets);
 
+/* exact_ftl.py:224-227 `_comparator_loss` (0.5 * sum |z @ x - y|) for B sequences in the
+ * reference's own operation order: OpenBLAS dgemv_t's row sums and NumPy's pairwise sum
+ * (DESIGN.md §4).  z [B][T][d], y [B][T] row-major, x [B][d] the comparator actions.
+ * The exact_ftl drop-in uses it for every RunResult.comp_loss. */
+int ocx_comparator_loss_blas_batch(const double* z, const double* y, const double* x, int64_t B,
+                                   int64_t T, int64_t d, double* comp_loss, int device);
+
 /* ---- float32 twin (algorithms.py, the module driver.py imports) ----------- */
 /* algorithms.py:28-54 simulate_alg (algo 0 FTRL, 1 FTL) and :65-120 simulate_SMART_like
  * (algo 2, thresh[B] = theta_thresh per sequence), batched over B sequences of float32 rows

@@ -84,6 +84,7 @@ SIGNATURES = {
     "ocx_gT_sweep": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double, c_int, c_dp, c_dp]),
     "ocx_gT_sweep_devices": (c_int, [c_i64p, c_int, c_i64, c_u64, c_i64, c_double,
                                      ctypes.POINTER(c_int), c_int, c_int, c_dp, c_dp]),
+    "ocx_comparator_loss_blas_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_int]),
     "ocx_twin32_batch": (c_int, [c_fp, c_fp, c_i64, c_i64, c_i64, c_int, c_double, c_dp, c_fp,
                                  c_dp, c_fp, c_i64p, c_int]),
     "ocx_dev_twin32": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp, c_vp,

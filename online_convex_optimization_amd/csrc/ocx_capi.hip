@@ -830,6 +830,32 @@ int ocx_gT_sweep(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed
                                 OCX_LANES_BEST, gmax, regrets);
 }
 
+int ocx_comparator_loss_blas_batch(const double* z, const double* y, const double* x, int64_t B,
+                                   int64_t T, int64_t d, double* comp_loss, int device) {
+    if (B < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative size");
+    if (B == 0) return OCX_OK;
+    if ((T * d > 0 && !z) || (T > 0 && !y) || (d > 0 && !x) || !comp_loss)
+        return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T), nx = (size_t)(B * d);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->cmp.ensure(nx * 8 + 8));
+    OCX_HIP(cx->at.ensure(ny * 8 + 8));
+    OCX_HIP(cx->out.ensure((size_t)B * 8));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    if (nx) OCX_HIP(hipMemcpyAsync(cx->cmp.p, x, nx * 8, hipMemcpyHostToDevice, st));
+    OCX_HIP(ocx_launch_comp_blas(cx->zraw.as<double>(), cx->yraw.as<double>(), cx->cmp.as<double>(),
+                                 B, T, d, cx->at.as<double>(), cx->out.as<double>(), st));
+    OCX_HIP(hipMemcpyAsync(comp_loss, cx->out.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
 // ---------------------------------------------------------------- float32 twin
 int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64_t d, int algo,
                      double eta0, const double* thresh, float* result, double* cum_loss,

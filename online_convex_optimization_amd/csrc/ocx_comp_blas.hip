@@ -1,0 +1,160 @@
+// ocx_comp_blas.hip — exact_ftl.py:224-227 `_comparator_loss`, 0.5 * sum |z @ x - y|, in
+// the operation order of the reference's own calls: OpenBLAS dgemv_t for z @ x and
+// NumPy's pairwise sum for .sum() (probed with the build container's OpenBLAS 0.3.29,
+// where the goldens were made; pinned against them, oracle.comparator_loss_blas_order):
+// * rows in groups of four (the 4x4 kernel): a 4-lane fma accumulation over the first
+//   m1 = d & ~3 coordinates, the lanes folded as (l0 + l2) + (l1 + l3);
+// * the T mod 4 last rows (the 4x1 kernel): 4-lane products added block after block;
+// * then the d mod 4 tail: 1 → fma(a0, x0, s); 2 → s + fma(a0, x0, a1 x1);
+//   3 → s + fma(a2, x2, fma(a0, x0, a1 x1));
+// * a one-row matrix (ddot): an fma chain for d < 16; 4 products per lane, folded
+//   ((a0 + a1) + a2) + a3 then (l0 + l2) + (l1 + l3), and an fma tail for 16 <= d < 32.
+// Rows of OpenBLAS's 4x2 kernel (T mod 4 >= 2, d >= 8) and one-row matrices with d >= 32
+// take the nearest of these orders (about one ulp per row).
+// Two launches: one thread per row (|q_t - y_t| into a scratch row), then one thread per
+// sequence for the pairwise sum (leaves of <= 128 with 8 accumulators, halves cut at
+// multiples of 8, per 8192-element buffer).  Used by the exact_ftl drop-in, whose
+// per-sequence calls are short; the batched engine keeps the kernels' sequential sums.
+#include <algorithm>
+
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+__device__ __forceinline__ double cb_fold(const double (&a)[4]) { return (a[0] + a[2]) + (a[1] + a[3]); }
+
+__device__ double cb_row(const double* __restrict__ r, const double* __restrict__ x, int64_t d,
+                         int64_t t, int64_t T) {
+    if (T == 1) {  // ddot
+        double s = 0.0;
+        if (d < 16) {
+            for (int64_t i = 0; i < d; ++i) s = fma(r[i], x[i], s);
+            return s;
+        }
+        double tot[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            tot[k] = ((r[k] * x[k] + r[4 + k] * x[4 + k]) + r[8 + k] * x[8 + k]) + r[12 + k] * x[12 + k];
+        s = cb_fold(tot);
+        for (int64_t i = 16; i < d; ++i) s = fma(r[i], x[i], s);
+        return s;
+    }
+    const int64_t m1 = d & ~(int64_t)3;
+    double s = 0.0;
+    if (m1) {
+        double acc[4];
+        if (t < 4 * (T / 4)) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = 0.0;
+            for (int64_t i = 0; i < m1; i += 4) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = fma(r[i + k], x[i + k], acc[k]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = r[k] * x[k];
+            for (int64_t i = 4; i < m1; i += 4) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = acc[k] + r[i + k] * x[i + k];
+            }
+        }
+        s = cb_fold(acc);
+    }
+    switch (d - m1) {
+        case 1: return fma(r[m1], x[m1], s);
+        case 2: return s + fma(r[m1], x[m1], r[m1 + 1] * x[m1 + 1]);
+        case 3: return s + fma(r[m1 + 2], x[m1 + 2], fma(r[m1], x[m1], r[m1 + 1] * x[m1 + 1]));
+        default: return s;
+    }
+}
+
+__global__ void ocx_comp_blas_rows_kernel(const double* __restrict__ z, const double* __restrict__ y,
+                                          const double* __restrict__ x, int64_t B, int64_t T,
+                                          int64_t d, double* __restrict__ absr) {
+    const int64_t n = B * T;
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = o / T, t = o - b * T;
+        absr[o] = fabs(cb_row(z + o * d, x + b * d, d, t, T) - y[o]);
+    }
+}
+
+constexpr int kCbBuf = 8192, kCbBlock = 128;
+
+__device__ double cb_leaf(const double* a, int m) {
+    if (m < 8) {
+        double s = -0.0;
+        for (int i = 0; i < m; ++i) s = s + a[i];
+        return s;
+    }
+    const int mf = m - (m & 7);
+    double r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r[k] = a[k];
+    for (int i = 8; i < mf; i += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = r[k] + a[i + k];
+    }
+    double s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = mf; i < m; ++i) s = s + a[i];
+    return s;
+}
+
+// NumPy's pairwise sum of one buffer (post order, a frame per pending right half)
+__device__ double cb_pairwise(const double* a, int nb) {
+    int fr_len[8];
+    double fr_val[8];
+    bool fr_has[8];
+    int sp = 0, m = nb, pos = 0;
+    for (;;) {
+        while (m > kCbBlock) {
+            int m2 = m / 2;
+            m2 -= m2 % 8;
+            fr_len[sp] = m - m2;
+            fr_has[sp] = false;
+            ++sp;
+            m = m2;
+        }
+        double v = cb_leaf(a + pos, m);
+        pos += m;
+        while (sp > 0 && fr_has[sp - 1]) {
+            v = fr_val[sp - 1] + v;
+            --sp;
+        }
+        if (sp == 0) return v;
+        fr_val[sp - 1] = v;
+        fr_has[sp - 1] = true;
+        m = fr_len[sp - 1];
+    }
+}
+
+__global__ void ocx_comp_blas_sum_kernel(const double* __restrict__ absr, int64_t B, int64_t T,
+                                         double* __restrict__ comp) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double* a = absr + b * T;
+    double tot = 0.0;
+    for (int64_t s0 = 0; s0 < T; s0 += kCbBuf) {
+        const int nb = (int)std::min<int64_t>(T - s0, kCbBuf);
+        const double p = cb_pairwise(a + s0, nb);
+        tot = s0 == 0 ? p : tot + p;
+    }
+    comp[b] = 0.5 * tot;
+}
+
+}  // namespace
+
+hipError_t ocx_launch_comp_blas(const double* z, const double* y, const double* x, int64_t B,
+                                int64_t T, int64_t d, double* absr, double* comp, hipStream_t st) {
+    if (B == 0) return hipSuccess;
+    const int64_t n = B * T;
+    if (n > 0) {
+        const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65536);
+        hipLaunchKernelGGL(ocx_comp_blas_rows_kernel, dim3(grid), dim3(256), 0, st, z, y, x, B, T,
+                           d, absr);
+    }
+    hipLaunchKernelGGL(ocx_comp_blas_sum_kernel, dim3((unsigned)((B + 63) / 64)), dim3(64), 0, st,
+                       absr, B, T, comp);
+    return hipGetLastError();
+}

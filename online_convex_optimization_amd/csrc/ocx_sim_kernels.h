@@ -59,3 +59,7 @@ hipError_t ocx_launch_twin32(const ocx_layout* L, const double* zt, const double
                              double* cum, float* comp, int64_t* sw, hipStream_t st);
 hipError_t ocx_launch_pack32(const ocx_layout* L, const float* z, const float* y, double* zt,
                              double* ytl, hipStream_t st);
+// exact_ftl.py:224-227 `_comparator_loss` in OpenBLAS / NumPy order (ocx_comp_blas.hip):
+// z [B][T][d] and y [B][T] row-major, x [B][d]; absr scratch [B][T]
+hipError_t ocx_launch_comp_blas(const double* z, const double* y, const double* x, int64_t B,
+                                int64_t T, int64_t d, double* absr, double* comp, hipStream_t st);

@@ -179,6 +179,16 @@ def compute_prefix_actions(solver, z: np.ndarray, y: np.ndarray) -> np.ndarray:
     return actions
 
 
+def _comparator_loss(z_arr, y_arr, x) -> float:
+    """exact_ftl.py:224-227 on the GPU, in the reference's operation order (dgemv_t row sums,
+    NumPy's pairwise sum; ocx_comparator_loss_blas_batch)."""
+    T, d = z_arr.shape
+    out = np.zeros(1)
+    _lib.call("ocx_comparator_loss_blas_batch", ptr(z_arr), ptr(y_arr),
+              ptr(_ensure_float64_contiguous(x)), 1, T, d, ptr(out), _fa._DEVICE)
+    return float(out[0])
+
+
 def _simulate_ftrl(z_arr, y_arr, *, eta0, comparator_action=None, comparator_solver=None,
                    norm="l2", solver_name=None, solver_opts=None) -> RunResult:
     """exact_ftl.py:230-277 on the GPU: the FTRL loop, then the comparator loss of the
@@ -198,8 +208,9 @@ def _simulate_ftrl(z_arr, y_arr, *, eta0, comparator_action=None, comparator_sol
     _lib.call("ocx_simulate_alg_batch", ptr(z_arr), ptr(y_arr), 1, T, d, 0, float(eta0),
               ptr(comp_vec), ptr(out[0:1]), ptr(out[1:2]), ptr(out[2:3]), ptr(x_last), _fa.EXACT,
               _fa._DEVICE)
-    return RunResult(cum_loss=float(out[1]), regret=float(out[0]), comp_loss=float(out[2]),
-                     x_last=x_last)
+    cum = float(out[1])
+    comp = _comparator_loss(z_arr, y_arr, comp_vec)
+    return RunResult(cum_loss=cum, regret=float(cum - comp), comp_loss=comp, x_last=x_last)
 
 
 def replay_exact_ftl(z: np.ndarray, y: np.ndarray, actions: np.ndarray) -> RunResult:
@@ -217,8 +228,9 @@ def replay_exact_ftl(z: np.ndarray, y: np.ndarray, actions: np.ndarray) -> RunRe
     comp = np.zeros(1)
     _lib.call("ocx_replay_batch", ptr(z_arr), ptr(y_arr), ptr(acts), 1, T, d, ptr(cum),
               ptr(comp), _fa._DEVICE)
-    return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - comp[0]),
-                     comp_loss=float(comp[0]), x_last=acts[T].copy())
+    c = _comparator_loss(z_arr, y_arr, acts[T])
+    return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - c), comp_loss=c,
+                     x_last=acts[T].copy())
 
 
 def _ftl_exact_gpu(z_arr, y_arr, norm) -> RunResult:
@@ -229,8 +241,9 @@ def _ftl_exact_gpu(z_arr, y_arr, norm) -> RunResult:
         raise ValueError("norm must be one of {'l2','linf','l1'}")
     cum, comp, act, _ = _engine.ftl_exact_batch(z_arr[None], y_arr[None], norm=norm,
                                                 lanes_per_seq=_fa.EXACT, device=_fa._DEVICE)
-    return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - comp[0]),
-                     comp_loss=float(comp[0]), x_last=act[0].copy())
+    c = _comparator_loss(z_arr, y_arr, act[0])
+    return RunResult(cum_loss=float(cum[0]), regret=float(cum[0] - c), comp_loss=c,
+                     x_last=act[0].copy())
 
 
 def simulate(z, y, *, algo: Literal["ftrl", "ftl_exact"] = "ftl_exact", eta0: float = 1.0,

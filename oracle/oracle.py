@@ -546,3 +546,112 @@ def t32_empirical_worst_case_thresholds(T_grid, *, runs: int = 5, base_seed: int
                 m = reg
         out[T] = m
     return out
+
+
+# ---------------------------------------------------------------------------
+# exact_ftl.py:224-227 `_comparator_loss` in explicit operation order
+# ---------------------------------------------------------------------------
+# z @ x - y goes to OpenBLAS dgemv_t (this image: 0.3.29, Haswell-class kernels); probed
+# and pinned against tests/golden (made by the reference itself):
+#   rows in groups of four (the 4x4 kernel): per row a 4-lane fma accumulation over the
+#     first m1 = d & ~3 coordinates, lanes summed as (l0 + l2) + (l1 + l3);
+#   the T mod 4 last rows (the 4x1 kernel): 4-lane products summed block after block with
+#     plain adds, the same lane fold;
+#   then the d mod 4 tail: 1 -> fma(a0, x0, s); 2 -> s + fma(a0, x0, a1 x1);
+#     3 -> s + fma(a2, x2, fma(a0, x0, a1 x1));
+#   a one-row matrix goes to ddot: an fma chain for d < 16, four 4-lane products folded
+#     ((a0 + a1) + a2) + a3, then (l0 + l2) + (l1 + l3) and an fma tail for 16 <= d < 32.
+# np.abs(r).sum(): NumPy's pairwise sum (float64, 8192-element buffers); then 0.5 * sum.
+from fractions import Fraction as _Fr  # noqa: E402
+
+
+def _fma64(a, b, c) -> float:
+    return float(_Fr(float(a)) * _Fr(float(b)) + _Fr(float(c)))
+
+
+def _dgemv_tail(s: float, a, x) -> float:
+    m3 = len(a)
+    if m3 == 1:
+        return _fma64(a[0], x[0], s)
+    if m3 == 2:
+        return s + _fma64(a[0], x[0], float(a[1]) * float(x[1]))
+    if m3 == 3:
+        return s + _fma64(a[2], x[2], _fma64(a[0], x[0], float(a[1]) * float(x[1])))
+    return s
+
+
+def dgemv_row(r, x, t: int, T: int) -> float:
+    """Row t of the T-row dgemv z @ x (see the block comment above)."""
+    d = len(r)
+    r = [float(v) for v in r]
+    x = [float(v) for v in x]
+    if T == 1:
+        if d < 16:
+            s = 0.0
+            for i in range(d):
+                s = _fma64(r[i], x[i], s)
+            return s
+        acc = [[r[4 * a + k] * x[4 * a + k] for k in range(4)] for a in range(4)]
+        tot = [((acc[0][k] + acc[1][k]) + acc[2][k]) + acc[3][k] for k in range(4)]
+        s = (tot[0] + tot[2]) + (tot[1] + tot[3])
+        for i in range(16, d):
+            s = _fma64(r[i], x[i], s)
+        return s
+    m1 = d & ~3
+    s = 0.0
+    if m1:
+        if t < 4 * (T // 4):
+            acc = [0.0] * 4
+            for i in range(0, m1, 4):
+                acc = [_fma64(r[i + k], x[i + k], acc[k]) for k in range(4)]
+        else:
+            acc = [r[k] * x[k] for k in range(4)]
+            for i in range(4, m1, 4):
+                acc = [acc[k] + r[i + k] * x[i + k] for k in range(4)]
+        s = (acc[0] + acc[2]) + (acc[1] + acc[3])
+    return _dgemv_tail(s, r[m1:], x[m1:])
+
+
+def _pw64_leaf(a) -> float:
+    n = len(a)
+    if n < 8:
+        s = -0.0
+        for v in a:
+            s = s + v
+        return s
+    m = n - n % 8
+    r = list(a[:8])
+    for i in range(8, m, 8):
+        r = [r[k] + a[i + k] for k in range(8)]
+    s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    for v in a[m:]:
+        s = s + v
+    return s
+
+
+def _pw64(a) -> float:
+    n = len(a)
+    if n <= 128:
+        return _pw64_leaf(a)
+    n2 = n // 2
+    n2 -= n2 % 8
+    return _pw64(a[:n2]) + _pw64(a[n2:])
+
+
+def sum64_numpy_order(a) -> float:
+    """np.sum of a contiguous float64 vector."""
+    a = [float(v) for v in a]
+    tot = None
+    for s in range(0, len(a), 8192):
+        p = _pw64(a[s:s + 8192])
+        tot = p if tot is None else tot + p
+    return 0.0 if tot is None else tot
+
+
+def comparator_loss_blas_order(z, y, x) -> float:
+    """exact_ftl.py:224-227 with every operation in the order OpenBLAS and NumPy use."""
+    z = _f64(z)
+    y = _f64(y)
+    T = z.shape[0]
+    r = [abs(dgemv_row(z[t], x, t, T) - float(y[t])) for t in range(T)]
+    return 0.5 * sum64_numpy_order(r)

@@ -38,7 +38,9 @@ def test_compute_prefix_actions_matches_oracle(ef, T, rep):
     fused = ef.run_ftl_exact(z, y)
     assert rp.cum_loss == fused.cum_loss == O.replay_cum_loss(z, y, want)
     assert rp.comp_loss == fused.comp_loss and np.array_equal(rp.x_last, fused.x_last)
-    assert rp.comp_loss == O.ftl_exact_closed_form(z, y)[1]
+    # comp_loss in exact_ftl's own order (dgemv_t rows, NumPy pairwise sum)
+    assert rp.comp_loss == O.comparator_loss_blas_order(z, y, want[T])
+    assert abs(rp.comp_loss - O.ftl_exact_closed_form(z, y)[1]) <= 1e-13 * max(1.0, rp.comp_loss)
 
 
 def test_append_row_and_prefix_solves_match(ef):
@@ -65,7 +67,8 @@ def test_run_ftrl_with_comparator_solver(ef):
         _, _, a, ok = O.ftl_exact_closed_form(z, y)
         assert ok
         ref = O.simulate_alg_full(z, y, 0, SQ2, comparator=a)
-        assert (rr.regret, rr.cum_loss, rr.comp_loss) == tuple(ref[:3]), run
+        cb = O.comparator_loss_blas_order(z, y, a)
+        assert (rr.regret, rr.cum_loss, rr.comp_loss) == (ref[1] - cb, ref[1], cb), run
         # the default (no solver, no action) builds its own solver: same result
         assert ef.run_ftrl(z, y, eta0=SQ2).regret == rr.regret
 
@@ -88,8 +91,9 @@ def test_exact_driver_loop_body(ef):
             ftl = ef.replay_exact_ftl(z_arr, y_arr, actions)
             c, p, a, ok = O.ftl_exact_closed_form(z_arr, y_arr)
             assert ok and np.array_equal(actions[-1], a)
-            assert ftl.regret == c - p
-            assert ftrl.regret == O.simulate_alg_full(z_arr, y_arr, 0, SQ2, comparator=a)[0]
+            cb = O.comparator_loss_blas_order(z_arr, y_arr, a)
+            assert ftl.regret == c - cb
+            assert ftrl.regret == O.simulate_alg_full(z_arr, y_arr, 0, SQ2, comparator=a)[1] - cb
 
 
 def test_out_of_regime_rejected(ef):
@@ -162,7 +166,8 @@ def test_poly_exact_ftl_matches_oracle(ef, norm):
         a0 = ef.compute_prefix_actions(s, z[0], y[0])
         assert np.array_equal(a0, ref[0][4])
         res = ef.run_ftl_exact(z[0], y[0], norm=norm)
-        assert (res.cum_loss, res.comp_loss) == (ref[0][0], ref[0][1])
+        assert (res.cum_loss, res.comp_loss) == (ref[0][0],
+                                                 O.comparator_loss_blas_order(z[0], y[0], ref[0][4][-1]))
 
 
 def test_poly_out_of_regime_rejected(ef):

@@ -75,13 +75,14 @@ def test_exact_ftl_golden(ocx, golden):
         r = rec["run_ftrl"]
         assert rr.cum_loss == F(r["cum_loss"]), name
         assert np.array_equal(rr.x_last, np.array([F(v) for v in r["x_last"]])), name
-        # comparator loss: reference uses BLAS dgemv + pairwise |r| sum, GPU a sequential sum
-        assert close(rr.comp_loss, F(r["comp_loss"]), 1e-13), name
-        assert close(rr.regret, F(r["regret"]), 1e-12), name
+        # comparator loss in the reference's order (dgemv_t rows, NumPy pairwise sum)
+        assert rr.comp_loss == F(r["comp_loss"]), name
+        assert rr.regret == F(r["regret"]), name
         acts = golden.arr(f"{name}__actions")
         rp = ef.replay_exact_ftl(z, y, acts)
         assert rp.cum_loss == F(rec["replay"]["cum_loss"]), name
-        assert close(rp.comp_loss, F(rec["replay"]["comp_loss"]), 1e-13), name
+        assert rp.comp_loss == F(rec["replay"]["comp_loss"]), name
+        assert rp.regret == F(rec["replay"]["regret"]), name
 
 
 def test_families_exact_ties(ocx, golden):
@@ -467,11 +468,14 @@ def test_ftl_exact_matches_oracle(ocx):
                 assert close([cum[b], comp[b]], [rc, rp]) and close(act[b], ra)
     res = ef.run_ftl_exact(z[0], y[0])
     rc, rp, ra, _ = O.ftl_exact_closed_form(z[0], y[0])
-    assert (res.cum_loss, res.comp_loss) == (rc, rp) and np.array_equal(res.x_last, ra)
+    cb = O.comparator_loss_blas_order(z[0], y[0], ra)  # the drop-in's comp_loss order
+    assert (res.cum_loss, res.comp_loss) == (rc, cb) and np.array_equal(res.x_last, ra)
+    assert close(cb, rp, 1e-13)
     rr = ef.run_ftrl(z[1], y[1], eta0=SQ2)
     _, _, a1, _ = O.ftl_exact_closed_form(z[1], y[1])
     ref = O.simulate_alg_full(z[1], y[1], 0, SQ2, comparator=a1)
-    assert (rr.regret, rr.cum_loss, rr.comp_loss) == ref[:3]
+    c1 = O.comparator_loss_blas_order(z[1], y[1], a1)
+    assert (rr.regret, rr.cum_loss, rr.comp_loss) == (ref[1] - c1, ref[1], c1)
     with pytest.raises(NotImplementedError):
         ef.run_ftl_exact(2.0 * z[0], y[0])
 
@@ -686,3 +690,23 @@ def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
     marked = np.arange(runs) % 3 == 0
     assert np.array_equal(mixed[marked], two[marked])
     assert np.array_equal(mixed[~marked], closed[~marked])
+
+
+@pytest.mark.parametrize("T,d", [(1, 3), (1, 20), (2, 8), (3, 5), (7, 13), (130, 5), (9000, 5),
+                                 (65, 64), (12, 1024)])
+def test_comparator_loss_blas_order(ocx, T, d):
+    """ocx_comparator_loss_blas_batch == the oracle's dgemv_t / pairwise order bit for bit
+    (pinned on the goldens in test_oracle_golden), and == NumPy on this host to 1e-15."""
+    from online_convex_optimization_amd import _lib
+    from online_convex_optimization_amd._lib import ptr
+    rng = np.random.default_rng(T * 7 + d)
+    B = 3
+    z = rng.standard_normal((B, T, d))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    x = rng.standard_normal((B, d))
+    got = np.zeros(B)
+    _lib.call("ocx_comparator_loss_blas_batch", ptr(z), ptr(y), ptr(x), B, T, d, ptr(got), 0)
+    for b in range(B):
+        if T * d <= 20000:
+            assert got[b] == O.comparator_loss_blas_order(z[b], y[b], x[b]), (T, d, b)
+        assert close(got[b], O.comparator_loss_blas(z[b], y[b], x[b]), 1e-15)

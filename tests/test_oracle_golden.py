@@ -45,8 +45,12 @@ def test_exact_ftl_run_ftrl_and_replay(golden):
         # the FTRL trajectory is the same op sequence → bit-exact
         assert cum == F(r["cum_loss"]), name
         assert np.array_equal(xl, np.array([F(v) for v in r["x_last"]])), name
-        # exact_ftl's comparator loss is BLAS dgemv + pairwise |r| sum
+        # exact_ftl's comparator loss is BLAS dgemv + pairwise |r| sum; the explicit-order
+        # restatement (what ocx_comp_blas.hip computes) reproduces it
         assert O.comparator_loss_blas(z, y, a) == F(r["comp_loss"]), name
+        assert O.comparator_loss_blas_order(z, y, a) == F(r["comp_loss"]), name
+        assert O.comparator_loss_blas_order(z, y, golden.arr(f"{name}__actions")[-1]) == \
+            F(rec["replay"]["comp_loss"]), name
         # the sequential comparator sum agrees to rounding
         assert comp == pytest.approx(F(r["comp_loss"]), rel=1e-13, abs=1e-12)
         acts = golden.arr(f"{name}__actions")
