@@ -56,6 +56,17 @@ __device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
     return (j & 1) ? zb[j >> 1].y : zb[j >> 1].x;
 }
 
+// Lane-local part of a tree total: the sequential sum of a lane's C products (with P = 1
+// the reference's order).  In-lane pairwise sums for P > 1 measured 1.5 % on the few-wave
+// T = 1e5 batch (profiles/r02_ab_lanesum.jsonl): not taken.
+template <int C>
+__device__ __forceinline__ double ocx_lane_sum(const double (&p)[C]) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc += p[j];
+    return acc;
+}
+
 
 // ---------------------------------------------------------------------------
 // Per-sequence totals of C per-lane products p[j] (coordinate c*C + j).
@@ -150,10 +161,7 @@ __device__ __forceinline__ void ocx_chain2_last(const double (&p)[C], const doub
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ double ocx_total(const double (&p)[C], int lane) {
     if constexpr (!CHAIN || P == 1) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < C; ++j) acc += p[j];
-        return ocx_seq_sum<P>(acc);
+        return ocx_seq_sum<P>(ocx_lane_sum<C>(p));
     } else if constexpr (P < OCX_CHAIN_WIDE_P) {
         // short chain: the hop's lane adds (exec-masked), one bpermute hands the total out
         const int c = lane % P;
@@ -197,14 +205,8 @@ template <int C, int P, bool CHAIN>
 __device__ __forceinline__ void ocx_total2(const double (&p)[C], const double (&q)[C], double& a,
                                            double& b, int lane) {
     if constexpr (!CHAIN || P == 1) {
-        double x = 0.0, y = 0.0;
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-            x += p[j];
-            y += q[j];
-        }
-        a = ocx_seq_sum<P>(x);
-        b = ocx_seq_sum<P>(y);
+        a = ocx_seq_sum<P>(ocx_lane_sum<C>(p));
+        b = ocx_seq_sum<P>(ocx_lane_sum<C>(q));
     } else if constexpr (P < OCX_CHAIN_WIDE_P) {
         const int c = lane % P;
         double x = 0.0, y = 0.0;
@@ -382,11 +384,10 @@ __device__ __forceinline__ double ocx_ftrl_q_sc(const double (&th)[C], const ocx
     return q;
 }
 
+// `sc` = −(η0/√t) (ocx_ftrl_scale: one sqrt/div per 64 steps instead of one per step)
 template <int C, int P, bool CHAIN>
-__device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const ocx_d2* z,
-                                                   int64_t t1, double eta0, double (&x)[C],
-                                                   int lane) {
-    const double sc = -(eta0 / sqrt((double)t1));
+__device__ __forceinline__ double ocx_ftrl_act_dot_sc(const double (&th)[C], const ocx_d2* z,
+                                                      double sc, double (&x)[C], int lane) {
     if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P) {
         double f;
         const double q = ocx_ftrl_q_sc<C, P, CHAIN>(th, z, sc, f, lane);
@@ -399,14 +400,14 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
     // products formed where they are summed: no p[]/pq[] arrays held across the sums
     double nsq, q;
     if constexpr (!CHAIN || P == 1) {
-        double a = 0.0, b = 0.0;
+        double pa[C], pb[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-            a += x[j] * x[j];
-            b += ocx_zj(z, j) * x[j];
+            pa[j] = x[j] * x[j];
+            pb[j] = ocx_zj(z, j) * x[j];
         }
-        nsq = ocx_seq_sum<P>(a);
-        q = ocx_seq_sum<P>(b);
+        nsq = ocx_seq_sum<P>(ocx_lane_sum<C>(pa));
+        q = ocx_seq_sum<P>(ocx_lane_sum<C>(pb));
     } else {
         // short chain: the hop's lane adds (exec-masked), one bpermute hands the totals out
         const int c = lane % P;
@@ -434,6 +435,13 @@ __device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const 
         q = ocx_zdot<C, P, CHAIN>(z, x, lane);
     }
     return q;
+}
+
+template <int C, int P, bool CHAIN>
+__device__ __forceinline__ double ocx_ftrl_act_dot(const double (&th)[C], const ocx_d2* z,
+                                                   int64_t t1, double eta0, double (&x)[C],
+                                                   int lane) {
+    return ocx_ftrl_act_dot_sc<C, P, CHAIN>(th, z, -(eta0 / sqrt((double)t1)), x, lane);
 }
 
 // Comparator loss Σ_t ½|z_t·xs − y_t| over steps [0, T) of one tile region, added to

@@ -493,6 +493,16 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     // offset w = f % (2P) of the sequence's segment in that plane, coordinate
     // j = (w/2)*C + 2k + (w%2)
     const int lg2P = __builtin_ctz((unsigned)(2 * P));
+    // P <= 32: store i of a row goes to plane k0 + i*kstep, offset w0, from ring slot
+    // j0 + i*jstep (see the DF = 1024 epilogue)
+    struct {
+        int w0, k0, kstep, j0, jstep;
+    } st1k;
+    st1k.w0 = lane & (2 * P - 1);
+    st1k.k0 = lane >> lg2P;
+    st1k.kstep = 64 >> lg2P;
+    st1k.j0 = (st1k.w0 >> 1) * C + 2 * st1k.k0 + (st1k.w0 & 1);
+    st1k.jstep = 2 * st1k.kstep;
     // rows leave the ring in batches of R: the sums of squares of a batch run side by
     // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
     const int R = LR ? 7 : batch_rows(d);
@@ -603,13 +613,26 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
                     const double scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
                     double* zrow = zt + (int64_t)g * T * 128 + t * 128 + (int64_t)s * 2 * P;
                     const int64_t kst = G * T * 128;
+                    if (P <= 32) {
+                        // 2P divides 64: the offset w is the lane's for every i and the plane
+                        // advances by 32/P per i, so the map is two strides (set up once per
+                        // kernel: st1k) instead of per-store index arithmetic; the ring holds
+                        // exactly this row (tailp is a multiple of 1024)
+                        const double* rp = ring + st1k.j0;
+                        double* zp = zrow + st1k.k0 * kst + st1k.w0;
+                        const int64_t pstep = st1k.kstep * kst;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            __builtin_nontemporal_store(rp[i * st1k.jstep] * scr, zp + i * pstep);
+                    } else {
 #pragma unroll 4
-                    for (int i = 0; i < 16; ++i) {
-                        const int f = i * 64 + lane;
-                        const int k = f >> lg2P, w = f & (2 * P - 1);
-                        const int j = (w >> 1) * C + 2 * k + (w & 1);
-                        __builtin_nontemporal_store(ring[(tailp + (unsigned)j) & rmask] * scr,
-                                                    zrow + k * kst + w);
+                        for (int i = 0; i < 16; ++i) {
+                            const int f = i * 64 + lane;
+                            const int k = f >> lg2P, w = f & (2 * P - 1);
+                            const int j = (w >> 1) * C + 2 * k + (w & 1);
+                            __builtin_nontemporal_store(ring[(tailp + (unsigned)j) & rmask] * scr,
+                                                        zrow + k * kst + w);
+                        }
                     }
                     tailp += (unsigned)d;
                     ++t;

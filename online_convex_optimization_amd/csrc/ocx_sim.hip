@@ -102,7 +102,12 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
 #pragma unroll
                         for (int j = 0; j < C; ++j) x[j] = (sc * th[j]) * fr;
                     } else {
+#ifdef OCX_ALG_STEP_SCALE  // tuning A/B: the scale's sqrt/div every step
                         q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t + 1, eta0, x, lane);
+#else
+                        const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);
+                        q = ocx_ftrl_act_dot_sc<C, P, CHAIN>(th, zb[u], sc, x, lane);
+#endif
                     }
                 } else {
                     if (exact && norm != 0) {

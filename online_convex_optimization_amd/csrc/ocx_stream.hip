@@ -96,7 +96,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                             double fr;
                             q = ocx_ftrl_q_sc<C, P, CHAIN>(th, zb[u], sc, fr, lane);
                         } else {
-                            q = ocx_ftrl_act_dot<C, P, CHAIN>(th, zb[u], t0 + t + 1, eta0, x, lane);
+                            const double sc = ocx_ftrl_scale(sct, t0 + t + 1, eta0, lane);
+                            q = ocx_ftrl_act_dot_sc<C, P, CHAIN>(th, zb[u], sc, x, lane);
                         }
                     } else {
                         ocx_action_ftl<C, P, CHAIN>(th, x, lane);

@@ -62,7 +62,11 @@ def gen1(args):
 
 def sweep(args):
     from online_convex_optimization_amd import engine
-    for T, runs in ((100, 1000000), (1000, 1000000), (10000, 131072), (100000, 131072)):
+    cases = ((100, 1000000), (1000, 1000000), (10000, 131072), (100000, 131072))
+    if args.Ts:
+        keep = {int(v) for v in args.Ts.split(",")}
+        cases = tuple(c for c in cases if c[0] in keep)
+    for T, runs in cases:
         engine.gT_regrets(T, runs, d=64, lanes_per_seq=args.lanes)  # warm (incl. HBM buffers)
         t0 = time.perf_counter()
         regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=args.lanes)
@@ -244,6 +248,7 @@ def smart(args):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--lanes", type=int, default=128, help="lanes_per_seq of the sweeps")
+    ap.add_argument("--Ts", default="", help="sweep: only these horizons (comma list)")
     ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget", "prof_long"])
     a = ap.parse_args()
     for w in a.what:
