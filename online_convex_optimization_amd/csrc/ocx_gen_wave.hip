@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "ocx_internal.h"
 #include "ocx_rng.h"
@@ -467,7 +468,11 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6);
+    // wave-uniform by construction; readfirstlane makes it provably so, and with it the
+    // stream index b: the per-stream SeedSequence hashing then runs on the scalar unit
+    // beside other waves' VALU work instead of on 64 identical lanes
+    const int64_t wave = __builtin_amdgcn_readfirstlane(
+        (int)(blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6)));
     if (wave >= nwaves) return;
     const int slot = rb + (d_arg > 128 ? kStackDoubles : 0);  // ring (+ pairwise stack)
     double* ring = rings + (threadIdx.x >> 6) * slot;
@@ -803,9 +808,20 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
         const int n = std::atoi(ev);
         if (n > 0 && n < cus) cus = n;
     }
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ocx_gen_wave_kernel<MODE, DF, LR, RAW>,
-                                                     kWaveBlock, lds);
-    if (e != hipSuccess) return e;
+    {
+        // the occupancy of an instance depends only on its LDS size here: query once
+        static std::mutex mu;
+        static size_t q_lds = ~(size_t)0;
+        static int q_per_cu = 0;
+        std::lock_guard<std::mutex> lk(mu);
+        if (q_lds != lds) {
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &q_per_cu, ocx_gen_wave_kernel<MODE, DF, LR, RAW>, kWaveBlock, lds);
+            if (e != hipSuccess) return e;
+            q_lds = lds;
+        }
+        per_cu = q_per_cu;
+    }
     int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
     // OCX_GEN_WAVES_PER_SIMD caps the resident generator waves (leaves registers free for
     // a kernel running beside it on another stream)
