@@ -156,6 +156,11 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
  * returns the R regrets (host array).  Only the regrets leave the GPU. */
 int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
                    double eta0, double* regrets, int lanes_per_seq, int device);
+/* ocx_gT_regrets reduced on device: *gmax = max(0.0, max over the R regrets) as
+ * fast_algorithms.py:228, :242-243 (bit-identical to the max of ocx_gT_regrets' output);
+ * only 8 bytes leave the GPU.  What empirical_worst_case_thresholds needs per T. */
+int ocx_gT_max(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
+               int lanes_per_seq, int device, double* gmax);
 /* In the bit-exact modes (lanes_per_seq 1 or -k) the comparator pass is the reference's
  * sequential sum; in the others the clipped-row closed form of ocx_dev_simulate_alg_ex
  * applies (the sampler's rows satisfy it by construction). */
@@ -164,7 +169,8 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
  * several GPUs of this process: for every T of T_grid [nT], the runs [0, runs) are split
  * into contiguous shards, one per device, each generated and simulated on its own GPU by a
  * host thread (ocx_gT_regrets).  gmax [nT] = max(0.0, max over runs) as :228,:242-243;
- * regrets [nT][runs] (nullable) in run order.  ngpus <= 0: every visible device. */
+ * regrets [nT][runs] (nullable: then each shard's max is reduced on its GPU, ocx_gT_max)
+ * in run order.  ngpus <= 0: every visible device. */
 int ocx_gT_sweep(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed, int64_t d,
                  double eta0, int ngpus, double* gmax, double* regrets);
 /* ocx_gT_sweep over an explicit device list (a device may repeat: its shards then share

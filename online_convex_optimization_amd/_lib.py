@@ -66,6 +66,7 @@ SIGNATURES = {
                                       c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_replay_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_dp, c_int]),
     "ocx_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp, c_int, c_int]),
+    "ocx_gT_max": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_int, c_int, c_dp]),
     "ocx_dev_pack": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_dev_gen_gT": (c_int, [ctypes.POINTER(Layout), c_u64, c_i64, c_vp, c_vp, c_vp]),
     "ocx_dev_gen_family": (c_int, [ctypes.POINTER(Layout), c_int, c_vp, c_vp, c_double, c_i64,

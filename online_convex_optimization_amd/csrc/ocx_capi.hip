@@ -1,6 +1,7 @@
 // ocx_capi.hip — the extern "C" boundary (include/ocx.h): layout planning, per-device
 // workspaces for the host entry points, argument checking and error reporting.
-// Host code only; kernels live in ocx_sim.hip / ocx_gen.hip.
+// Host code, plus the g(T) max fold below; the other kernels live in ocx_sim.hip /
+// ocx_gen*.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -67,6 +68,7 @@ struct DevCtx {
     hipStream_t stream = nullptr;
     DevBuf zraw, yraw, zt, yt, at, araw, cmp, thr, out, sw;
     DevBuf rstate, lstate, theta, acc;  // long-horizon (T-chunked) g(T) sweep
+    DevBuf gmax;                        // ocx_gT_max: the running max's bit pattern
 };
 
 DevCtx g_ctx[kMaxDevices];
@@ -94,6 +96,34 @@ int ctx_enter(int device, DevCtx** out) {
 }
 
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// g(T) = max over runs of the regrets, starting from 0.0 with `reg > max`
+// (fast_algorithms.py:228, :242-243).  Every candidate that can win is > +0.0 (a NaN never
+// passes `>`), and positive doubles order as their bit patterns, so blocks and batches fold
+// into *acc (initialised to +0.0) by a 64-bit unsigned atomic max: a selection, bit-identical
+// to the host's loop over the same regrets.
+__global__ void ocx_max_fold_kernel(const double* __restrict__ r, int64_t n,
+                                    unsigned long long* __restrict__ acc) {
+    double m = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const double v = r[i];
+        if (v > m) m = v;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const double u = __shfl_down(m, o, 64);
+        if (u > m) m = u;
+    }
+    if ((threadIdx.x & 63) == 0 && m > 0.0)
+        atomicMax(acc, (unsigned long long)__double_as_longlong(m));
+}
+
+hipError_t launch_max_fold(const double* r, int64_t n, unsigned long long* acc, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(ocx_max_fold_kernel, dim3(grid), dim3(256), 0, st, r, n, acc);
+    return hipGetLastError();
+}
 
 int even_supported_C(int64_t need) {
     static const int Cs[] = {2, 4, 6, 8, 12, 16, 24, 32, 48, 64};
@@ -134,7 +164,7 @@ int ocx_release_buffers(int device) {
     OCX_HIP(hipStreamSynchronize(cx->stream));
     for (DevBuf* b : {&cx->zraw, &cx->yraw, &cx->zt, &cx->yt, &cx->at, &cx->araw, &cx->cmp,
                       &cx->thr, &cx->out, &cx->sw, &cx->rstate, &cx->lstate, &cx->theta,
-                      &cx->acc})
+                      &cx->acc, &cx->gmax})
         OCX_HIP(b->release());
     return OCX_OK;
 }
@@ -624,11 +654,18 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
     return OCX_OK;
 }
 
-int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
-                   double eta0, double* regrets, int lanes_per_seq, int device) {
+}  // extern "C"
+
+namespace {
+
+// fast_algorithms.py:230-243 for one T: the regrets of runs [run0, run0 + R) to the host
+// (`regrets`), or only their max (`gmax`: the regrets never leave the GPU).
+int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
+           double* regrets, double* gmax, int lanes_per_seq, int device) {
     if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
+    if (gmax) *gmax = 0.0;
     if (R == 0) return OCX_OK;
-    if (!regrets) return fail(OCX_E_INVALID, "NULL regrets");
+    if (!regrets && !gmax) return fail(OCX_E_INVALID, "NULL regrets");
     // the sampler's rows are clipped: outside the bit-exact modes the comparator loss
     // takes the closed form (ocx_dev_simulate_alg_ex), one HBM pass instead of two
     const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
@@ -636,6 +673,20 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);
     hipStream_t st = cx->stream;
+    unsigned long long* dmax = nullptr;
+    if (!regrets) {
+        OCX_HIP(cx->gmax.ensure(8));
+        dmax = cx->gmax.as<unsigned long long>();
+        OCX_HIP(hipMemsetAsync(dmax, 0, 8, st));  // +0.0
+    }
+    // the max leaves the GPU once, after the last batch
+    auto finish = [&]() -> int {
+        if (dmax) {
+            OCX_HIP(hipMemcpyAsync(gmax, dmax, 8, hipMemcpyDeviceToHost, st));
+            OCX_HIP(hipStreamSynchronize(st));
+        }
+        return OCX_OK;
+    };
     // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB): by default 90 % of
     // what is free plus what this context already holds, at most 240 GiB.  Long horizons
     // run few-wave, latency-bound batches, so a batch's time hardly grows with its size:
@@ -703,11 +754,15 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
             OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
                                    cx->out.as<double>(), nullptr, nullptr, nullptr, st, nullptr,
                                    nullptr, onepass));
-            OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8,
-                                   hipMemcpyDeviceToHost, st));
-            OCX_HIP(hipStreamSynchronize(st));
+            if (dmax) {
+                OCX_HIP(launch_max_fold(cx->out.as<double>(), nb, dmax, st));
+            } else {
+                OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8,
+                                       hipMemcpyDeviceToHost, st));
+                OCX_HIP(hipStreamSynchronize(st));
+            }
         }
-        return OCX_OK;
+        return finish();
     }
     // streamed: batches of kBatch runs, horizon cut into chunks of Tc steps
     // (ocx_stream.hip): seek → pass A (generate chunk, advance theta) → pass B
@@ -777,10 +832,30 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
                                              unclean));
             }
         }
-        OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
-        OCX_HIP(hipStreamSynchronize(st));
+        if (dmax) {
+            OCX_HIP(launch_max_fold(reg, nb, dmax, st));
+        } else {
+            OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
+            OCX_HIP(hipStreamSynchronize(st));
+        }
     }
-    return OCX_OK;
+    return finish();
+}
+
+}  // namespace
+
+extern "C" {
+
+int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                   double eta0, double* regrets, int lanes_per_seq, int device) {
+    if (!regrets && R > 0) return fail(OCX_E_INVALID, "NULL regrets");
+    return gT_run(base_seed, T, run0, R, d, eta0, regrets, nullptr, lanes_per_seq, device);
+}
+
+int ocx_gT_max(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
+               int lanes_per_seq, int device, double* gmax) {
+    if (!gmax) return fail(OCX_E_INVALID, "NULL gmax");
+    return gT_run(base_seed, T, run0, R, d, eta0, nullptr, gmax, lanes_per_seq, device);
 }
 
 int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t base_seed,
@@ -791,16 +866,17 @@ int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t b
     if (!T_grid || !gmax || !devices || ndev < 1) return fail(OCX_E_INVALID, "NULL argument");
     for (int i = 0; i < nT; ++i)
         if (T_grid[i] < 0) return fail(OCX_E_INVALID, "negative T");
-    std::vector<double> tmp(regrets ? 0 : (size_t)runs);
     for (int i = 0; i < nT; ++i) {
-        double* row = regrets ? regrets + (size_t)i * runs : tmp.data();
+        // without `regrets` each shard reduces its max on its GPU and only that leaves it
+        double* row = regrets ? regrets + (size_t)i * runs : nullptr;
+        std::vector<double> smax(ndev, 0.0);
         // contiguous shards [runs*k/ndev, runs*(k+1)/ndev), one host thread per shard
         std::vector<int> rc(ndev, OCX_OK);
         std::vector<std::string> err(ndev);
         auto work = [&](int k) {
             const int64_t lo = runs * k / ndev, hi = runs * (k + 1) / ndev;
-            rc[k] = ocx_gT_regrets(base_seed, T_grid[i], lo, hi - lo, d, eta0, row + lo,
-                                   lanes_per_seq, devices[k]);
+            rc[k] = gT_run(base_seed, T_grid[i], lo, hi - lo, d, eta0, row ? row + lo : nullptr,
+                           row ? nullptr : &smax[k], lanes_per_seq, devices[k]);
             if (rc[k]) err[k] = g_err;  // the message is thread-local
         };
         std::vector<std::thread> th;
@@ -810,8 +886,13 @@ int ocx_gT_sweep_devices(const int64_t* T_grid, int nT, int64_t runs, uint64_t b
         for (int k = 0; k < ndev; ++k)
             if (rc[k]) return fail(rc[k], "device " + std::to_string(devices[k]) + ": " + err[k]);
         double m = 0.0;  // fast_algorithms.py:228, :242-243
-        for (int64_t r = 0; r < runs; ++r)
-            if (row[r] > m) m = row[r];
+        if (row) {
+            for (int64_t r = 0; r < runs; ++r)
+                if (row[r] > m) m = row[r];
+        } else {
+            for (int k = 0; k < ndev; ++k)
+                if (smax[k] > m) m = smax[k];
+        }
         gmax[i] = m;
     }
     return OCX_OK;

@@ -272,18 +272,31 @@ def max_regret(regrets: np.ndarray) -> float:
     return float(pos.max()) if pos.size else 0.0
 
 
+def gT_max(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float = SQRT2,
+           run0: int = 0, lanes_per_seq: int = LANES_BEST, device: int = 0) -> float:
+    """max(0, max of gT_regrets(...)) reduced on device (``ocx_gT_max``): the regrets never
+    leave the GPU (fast_algorithms.py:228, :242-243)."""
+    if base_seed < 0 or base_seed >= 2 ** 64:
+        raise ValueError("base_seed must be in [0, 2**64)")
+    out = np.zeros(1)
+    _lib.call("ocx_gT_max", int(base_seed), int(T), int(run0), int(runs), int(d), float(eta0),
+              int(lanes_per_seq), int(device), ptr(out))
+    return float(out[0])
+
+
 def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5,
              eta0: float = SQRT2, devices: Optional[Sequence[int]] = None,
-             lanes_per_seq: int = LANES_BEST) -> dict:
+             lanes_per_seq: int = LANES_BEST, return_regrets: bool = True) -> dict:
     """empirical_worst_case_thresholds on one or several GPUs of this process
     (``ocx_gT_sweep_devices``).
 
     For every T the runs are split into contiguous shards, one per device, each generated
     and simulated on its own GPU by a native host thread; the per-shard regrets land in
-    run order.  Returns {T: (g(T), regrets[runs])}."""
+    run order.  Returns {T: (g(T), regrets[runs])}; with ``return_regrets=False`` each
+    shard's max is reduced on its GPU and the regrets entry is None."""
     devs = [int(v) for v in devices] if devices else [0]
     grid = np.ascontiguousarray([int(T) for T in T_grid], dtype=np.int64)
-    regs = np.zeros((len(grid), int(runs)), dtype=np.float64)
+    regs = np.zeros((len(grid), int(runs)), dtype=np.float64) if return_regrets else None
     gmax = np.zeros(len(grid), dtype=np.float64)
     dv = (ctypes.c_int * len(devs))(*devs)
     if base_seed < 0 or base_seed >= 2 ** 64:
@@ -291,7 +304,8 @@ def gT_sweep(T_grid: Sequence[int], runs: int, *, base_seed: int = 0, d: int = 5
     _lib.call("ocx_gT_sweep_devices", grid.ctypes.data_as(_lib.c_i64p), len(grid), int(runs),
               int(base_seed), int(d), float(eta0), dv, len(devs), int(lanes_per_seq),
               ptr(gmax), ptr(regs))
-    return {int(T): (float(gmax[i]), regs[i]) for i, T in enumerate(grid)}
+    return {int(T): (float(gmax[i]), regs[i] if regs is not None else None)
+            for i, T in enumerate(grid)}
 
 
 # ---------------------------------------------------------------------------

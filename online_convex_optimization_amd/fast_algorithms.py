@@ -114,7 +114,7 @@ def empirical_worst_case_thresholds(
     for T_val in it:
         T = int(T_val)
         res = engine.gT_sweep([T], int(runs), base_seed=int(base_seed), d=int(d), eta0=SQRT2,
-                              devices=devs, lanes_per_seq=EXACT)
+                              devices=devs, lanes_per_seq=EXACT, return_regrets=False)
         g_emp[T] = res[T][0]
     return g_emp
 

@@ -99,3 +99,27 @@ def test_gT_sweep_device_list(reference):
         g, regs = out[T]
         assert np.array_equal(regs, reference[T])
         assert g == max(0.0, float(reference[T].max()))
+
+
+def test_gT_max_on_device(reference):
+    """ocx_gT_max / gT_sweep(return_regrets=False): the max reduced on device (an atomic max
+    over bit patterns) equals the max of the regrets the host receives, bit for bit, on one
+    device, on a device list, and through the streamed (T-chunked) path."""
+    from online_convex_optimization_amd import engine
+    for T in T_GRID:
+        want = max(0.0, float(reference[T].max()))
+        assert engine.gT_max(T, RUNS, base_seed=3, d=D) == want
+        # ragged shards of one run range
+        assert max(engine.gT_max(T, 20, base_seed=3, d=D),
+                   engine.gT_max(T, RUNS - 20, base_seed=3, d=D, run0=20)) == want
+    out = engine.gT_sweep(T_GRID, RUNS, base_seed=3, d=D, devices=[0, 0], return_regrets=False)
+    for T in T_GRID:
+        g, regs = out[T]
+        assert regs is None and g == max(0.0, float(reference[T].max()))
+    os.environ["OCX_HBM_BUDGET_GB"] = "0.0004"  # forces the streamed path (T-chunks)
+    try:
+        for T in T_GRID:
+            assert engine.gT_max(T, RUNS, base_seed=3, d=D) == max(0.0, float(reference[T].max()))
+    finally:
+        del os.environ["OCX_HBM_BUDGET_GB"]
+    assert engine.gT_max(T_GRID[0], 0, base_seed=3, d=D) == 0.0

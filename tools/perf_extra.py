@@ -71,9 +71,17 @@ def sweep(args):
         t0 = time.perf_counter()
         regs = engine.gT_regrets(T, runs, d=64, lanes_per_seq=args.lanes)
         dt = time.perf_counter() - t0
+        # what empirical_worst_case_thresholds needs per T: g(T) only, reduced on device
+        engine.gT_max(T, runs, d=64, lanes_per_seq=args.lanes)
+        t0 = time.perf_counter()
+        g = engine.gT_max(T, runs, d=64, lanes_per_seq=args.lanes)
+        dm = time.perf_counter() - t0
+        assert g == engine.max_regret(regs)
         print(json.dumps({"what": "gT_sweep", "T": T, "runs": runs, "d": 64, "lanes": args.lanes,
                           "seconds": dt, "timesteps_per_s": T * runs / dt,
                           "frac_1040B": T * runs / dt * 1040 / 8e12,
+                          "gmax_seconds": dm, "gmax_timesteps_per_s": T * runs / dm,
+                          "gmax_frac_1040B": T * runs / dm * 1040 / 8e12,
                           "g": engine.max_regret(regs)}), flush=True)
 
 
