@@ -474,7 +474,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     const int64_t wave = __builtin_amdgcn_readfirstlane(
         (int)(blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6)));
     if (wave >= nwaves) return;
-    const int slot = rb + (d_arg > 128 ? kStackDoubles : 0);  // ring (+ pairwise stack)
+    const int slot = rb + (DF == 0 && d_arg > 128 ? kStackDoubles : 0);  // ring (+ pairwise stack)
     double* ring = rings + (threadIdx.x >> 6) * slot;
     PwFrame* stk = reinterpret_cast<PwFrame*>(ring + rb);
     const int rmask = rb - 1;
@@ -492,7 +492,6 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     }
     const int d = DF ? DF : d_arg;
     const int S = 64 / P;
-    constexpr bool W1K = (DF == 1024);
     const int Dp = DF == 64 ? 64 : P * C;
     // DF = 1024 store map: flat index f = i*64 + lane of the row → plane k = f / (2P),
     // offset w = f % (2P) of the sequence's segment in that plane, coordinate
@@ -586,6 +585,63 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
                     t += nrows;
                 }
             }
+        } else if constexpr (MODE == 0 && DF == 1024) {
+            // d = 1024: full rounds (no need cap at the row's end).  The row always starts
+            // at ring[0]; a round that completes it spills at most 63 normals of the next
+            // row into ring[1024, 1087), which move to the front once the row has left.
+            // (The ring is 1088 doubles: 4 waves' rings and the tables fill 160 KiB of LDS
+            // with four 256-thread blocks, so the occupancy of the 1024 ring is kept.)
+            constexpr int kFlat = 2047;  // every ring index is < 1088: masking is a no-op
+            const uint32_t total = (uint32_t)(T * 1024);
+            uint32_t produced = 0;
+            unsigned head = 0;
+            int64_t t = 0;
+            const int64_t kst = G * T * 128;
+            const double* rp = ring + st1k.j0;
+            const int64_t pstep = st1k.kstep * kst;
+            while (produced < total) {
+                const uint32_t left = total - produced;
+                const int n = left >= 64u
+                                  ? zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane)
+                                  : zig_round<true>(w, (int)left, tb, ring, kFlat, head, lane);
+                produced += (uint32_t)n;
+                head += (unsigned)n;
+                if (head >= 1024u) {
+                    // NumPy's pairwise sum of squares: lanes 8l..8l+7 keep leaf l's eight
+                    // accumulators (16 values each), the 64 partials combine in its order
+                    const unsigned o = (unsigned)((lane >> 3) * 128 + (lane & 7));
+                    double v[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) v[q] = ring[o + 8u * q];
+                    double acc = v[0] * v[0];
+#pragma unroll
+                    for (int q = 1; q < 16; ++q) acc += v[q] * v[q];
+                    const double nrm = sqrt(ocx_seq_sum<64>(acc));
+                    const double scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
+                    double* zrow = zt + (int64_t)g * T * 128 + t * 128 + (int64_t)s * 2 * P;
+                    if (P <= 32) {
+                        double* zp = zrow + st1k.k0 * kst + st1k.w0;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            __builtin_nontemporal_store(rp[i * st1k.jstep] * scr, zp + i * pstep);
+                    } else {
+#pragma unroll 4
+                        for (int i = 0; i < 16; ++i) {
+                            const int f = i * 64 + lane;
+                            const int k = f >> lg2P, wo = f & (2 * P - 1);
+                            const int j = (wo >> 1) * C + 2 * k + (wo & 1);
+                            __builtin_nontemporal_store(ring[j] * scr, zrow + k * kst + wo);
+                        }
+                    }
+                    // the spill moves to the front (LDS operations of a wave run in order:
+                    // the row's reads above complete before these writes)
+                    const unsigned ov = head - 1024u;
+                    const double sp = ring[1024 + (lane < 63 ? lane : 63)];
+                    if ((unsigned)lane < ov) ring[lane] = sp;
+                    head = ov;
+                    ++t;
+                }
+            }
         } else {
         const int64_t rows = (MODE == 0) ? T : T_seed;
         uint32_t remaining = (uint32_t)(rows * d);  // normals still to draw (< 2^32, host-checked)
@@ -595,7 +651,6 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
         int64_t t = 0;
         while (remaining > 0) {
             int need = remaining < 64 ? (int)remaining : 64;
-            if (W1K && MODE == 0 && need > d - (int)partial) need = d - (int)partial;
             const int n = zig_round<MODE == 0>(w, need, tb, ring, rmask, head, lane);
             head += n;
             remaining -= (uint32_t)n;
@@ -604,46 +659,6 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             while (partial >= (unsigned)d) {
                 partial -= (unsigned)d;
                 ++ready;
-            }
-            if constexpr (W1K && MODE == 0) {
-                if (ready) {  // one whole row in the ring, starting at tailp
-                    const unsigned o = tailp + (unsigned)((lane >> 3) * 128 + (lane & 7));
-                    double v[16];
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) v[q] = ring[(o + 8u * q) & rmask];
-                    double acc = v[0] * v[0];
-#pragma unroll
-                    for (int q = 1; q < 16; ++q) acc += v[q] * v[q];
-                    const double nrm = sqrt(ocx_seq_sum<64>(acc));
-                    const double scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
-                    double* zrow = zt + (int64_t)g * T * 128 + t * 128 + (int64_t)s * 2 * P;
-                    const int64_t kst = G * T * 128;
-                    if (P <= 32) {
-                        // 2P divides 64: the offset w is the lane's for every i and the plane
-                        // advances by 32/P per i, so the map is two strides (set up once per
-                        // kernel: st1k) instead of per-store index arithmetic; the ring holds
-                        // exactly this row (tailp is a multiple of 1024)
-                        const double* rp = ring + st1k.j0;
-                        double* zp = zrow + st1k.k0 * kst + st1k.w0;
-                        const int64_t pstep = st1k.kstep * kst;
-#pragma unroll
-                        for (int i = 0; i < 16; ++i)
-                            __builtin_nontemporal_store(rp[i * st1k.jstep] * scr, zp + i * pstep);
-                    } else {
-#pragma unroll 4
-                        for (int i = 0; i < 16; ++i) {
-                            const int f = i * 64 + lane;
-                            const int k = f >> lg2P, w = f & (2 * P - 1);
-                            const int j = (w >> 1) * C + 2 * k + (w & 1);
-                            __builtin_nontemporal_store(ring[(tailp + (unsigned)j) & rmask] * scr,
-                                                        zrow + k * kst + w);
-                        }
-                    }
-                    tailp += (unsigned)d;
-                    ++t;
-                    ready = 0;
-                }
-                continue;
             }
             while (ready >= R || (remaining == 0 && ready > 0)) {
                 const int nrows = ready < R ? ready : R;
@@ -781,7 +796,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
 namespace {
 
 int ring_doubles(int64_t d, int DF, bool LR = false) {
-    if (DF == 1024) return 1024;  // exactly one row: rounds stop at the row's end
+    if (DF == 1024) return 1024 + 64;  // one row + the next row's first round (ocx_gen_wave_kernel)
     if (LR) return 512;           // 7 rows + one round's normals (ocx_gen_wave_kernel, LR)
     // a full batch of rows plus one round of normals
     int rb = 128;
@@ -796,7 +811,7 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
                           const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
     const int rb = (MODE == 0) ? ring_doubles(d, DF, LR) : 0;
     const size_t lds =
-        (MODE == 0) ? (size_t)(rb + (d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
+        (MODE == 0) ? (size_t)(rb + (DF == 0 && d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
     // resident waves: fill the GPU once, sequences spread evenly over the waves
     int dev = 0, cus = 256, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
