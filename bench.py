@@ -43,8 +43,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    # 200 x 26.5 ms: a 5 s timed window, long enough for a once-every-few-seconds GPU-busy
+    # sampler to see the kernel running (the CPU-baseline leg takes most of the run)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--B", type=int, default=32768, help="sequences per GPU (resident batch)")
     ap.add_argument("--T", type=int, default=10000)
     ap.add_argument("--d", type=int, default=64)
@@ -61,7 +63,7 @@ def parse():
                     help="launches of the two-pass kernel timed after the metric for the "
                          "two_pass comparison (0 disables; profile runs use 0 so every "
                          "ocx_alg_kernel launch in the trace is the default one)")
-    ap.add_argument("--e2e-steps", type=int, default=3,
+    ap.add_argument("--e2e-steps", type=int, default=10,
                     help="untimed-for-the-metric batches of generation + simulation reported "
                          "as end_to_end (0 disables)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
