@@ -125,3 +125,18 @@ def test_untile_roundtrip_matches_pack_formula():
         ok = b < B
         yt[ok] = y[b[ok], t[ok]]
         assert np.array_equal(untile_y(yt, L), y)
+
+
+def test_positive_double_bit_patterns_order_as_values():
+    """ocx_gT_max folds regrets with a 64-bit unsigned atomic max over their bit patterns
+    (csrc/ocx_capi.hip ocx_max_fold_kernel): only values > +0.0 reach it, and for those
+    (subnormals, normals, +inf) the unsigned order of the patterns is the order of the
+    values, so the fold selects the same element as fast_algorithms.py:242-243's `>` loop."""
+    rng = np.random.default_rng(7)
+    v = np.abs(rng.standard_normal(20000)) * 10.0 ** rng.integers(-320, 300, 20000)
+    v = np.concatenate([v[v > 0.0], [5e-324, 2.2250738585072014e-308, 1.0, np.inf]])
+    bits = v.view(np.uint64)
+    order_v = np.argsort(v, kind="stable")
+    order_b = np.argsort(bits, kind="stable")
+    assert np.array_equal(v[order_v], v[order_b])
+    assert v[np.argmax(bits)] == v.max()
