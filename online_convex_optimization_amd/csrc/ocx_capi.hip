@@ -741,6 +741,25 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
                 nbat = (R + chunk - 1) / chunk;
                 chunk = (R + nbat - 1) / nbat;
             }
+            // Whole generator rounds: with many streams per generator wave (a batch over
+            // twice the generator's resident waves, 16 per CU) the streams of a batch
+            // spread as ceil(batch / waves) per wave, and the part of the last round left
+            // empty is lost.  One batch more is taken when it wastes less (by more than
+            // the ~1 % an extra batch costs): d = 64, T = 1e4, 131 072 runs as three
+            // batches of 43 691 (11 streams per wave, 3 % idle) took 398.8 ms, as four of
+            // 32 768 (8 per wave) 386.5 ms; T = 1e3, 1e6 runs keeps its three
+            // (profiles/r02_batch_budget.jsonl).
+            const int64_t rs = (int64_t)cus * 16;
+            auto idle = [rs](int64_t c) {
+                return (double)(((c + rs - 1) / rs) * rs) / (double)c - 1.0;
+            };
+            if (nbat >= 2 && chunk > 2 * rs) {
+                const int64_t c2 = (R + nbat) / (nbat + 1);  // ceil(R / (nbat + 1))
+                if (idle(c2) + 0.01 < idle(chunk)) {
+                    ++nbat;
+                    chunk = c2;
+                }
+            }
         }
         OCX_HIP(cx->out.ensure((size_t)chunk * 8));
         for (int64_t r0 = 0; r0 < R; r0 += chunk) {
