@@ -1,4 +1,6 @@
 #!/bin/bash
+# ROUND 1 (two-pass comparator default). For the closed-form default use tools/gpu_final_r02.sh:
+# this script times and counts every ocx_alg_kernel launch, two-pass ones included.
 # End-of-round evidence for the bench kernel: smoke(), kernel-trace stats of the default
 # bench command, and the two PMC HBM passes (FETCH_SIZE, WRITE_SIZE) -> traffic.json.
 set -u
