@@ -28,16 +28,27 @@
  *              sequential order, so results are bit-identical;
  *       -k     exact with k lanes; for k > 1 the running sum is handed from lane to
  *              lane (layout.chain = 1);
- *       OCX_LANES_BEST (128)  per workload: the exact layout (value 1) wherever its
- *              lane chains are short (fewer than 8 lanes per sequence), where the
- *              kernels stream at the HBM roofline; butterfly sums otherwise (d >= 512,
- *              or few-wave batches such as the capacity-limited T = 1e5 g(T) batch),
- *              where a chain of 8+ lanes leaves the kernel latency-bound.  Results are
- *              bit-identical where the exact layout is kept, ~1e-16 relative elsewhere.
+ *       OCX_LANES_BEST (128)  the fastest certified mode, the default of the batched
+ *              APIs: the exact layout's sums (value 1) wherever its lane chains are short
+ *              (fewer than 8 lanes per sequence), where the kernels stream at the HBM
+ *              roofline; butterfly sums otherwise (d >= 512, or few-wave batches such as
+ *              the capacity-limited T = 1e5 g(T) batch), where a chain of 8+ lanes leaves
+ *              the kernel latency-bound.  The g(T) and FTRL-vs-exact entry points also
+ *              take the closed-form comparator losses in this mode wherever the kernel
+ *              certifies them (ocx_dev_simulate_alg_ex), so their results are NOT
+ *              bit-identical to the reference: the loops keep the sums above, the
+ *              comparator loss differs from the reference's sequential sum by that sum's
+ *              rounding (about 1e-13 relative on the regret at T = 1e4).  Use 1 (or -k)
+ *              for bit-identical results: every drop-in module does.
  */
-#define OCX_LANES_BEST 128
 #ifndef OCX_H_
 #define OCX_H_
+
+#define OCX_LANES_BEST 128
+/* ocx_version() == OCX_VERSION = 10000 * major + 100 * minor + patch (200 = 0.2.0).  0.2.0:
+ * ocx_ftrl_vs_exact_batch has its round-1 signature again (the `norm` argument moved to
+ * ocx_ftrl_vs_exact_batch_ex); callers built against 0.1.x check ocx_version() >= 200. */
+#define OCX_VERSION 200
 
 #include <stddef.h>
 #include <stdint.h>
@@ -142,8 +153,15 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
  * (int32, required; see ocx_ftl_exact_batch). */
 int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                            double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
+                            double* comp_ftl, double* cmp_action, int32_t* regime,
                             int lanes_per_seq, int device);
+/* ocx_ftrl_vs_exact_batch over the unit ball of `norm` (0 l2 — what the plain entry point
+ * uses —, 1 l1, 2 linf), as ocx_ftl_exact_batch.  (Version 200 restored the plain entry
+ * point's round-1 signature; `norm` lives here.) */
+int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                               double eta0, double* cum_ftrl, double* cum_exact,
+                               double* comp_exact, double* comp_ftl, double* cmp_action,
+                               int32_t* regime, int norm, int lanes_per_seq, int device);
 
 /* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
  * cum_loss = sum_{t<T} 0.5|z_t.a_t - y_t|; comp_loss = sum_t 0.5|z_t.a_T - y_t|. */
@@ -156,14 +174,20 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
  * returns the R regrets (host array).  Only the regrets leave the GPU. */
 int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
                    double eta0, double* regrets, int lanes_per_seq, int device);
+/* ocx_gT_regrets with the regrets written to device memory: regrets_dev [R] lives on
+ * `device`.  Nothing crosses PCIe (the FTRL kernel writes each batch's regrets in place);
+ * the call returns when they are complete, so any stream or collective (an RCCL all-gather
+ * of every rank's shard, parallel.gT_sweep_distributed) may read them afterwards. */
+int ocx_gT_regrets_dev(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                       double eta0, double* regrets_dev, int lanes_per_seq, int device);
 /* ocx_gT_regrets reduced on device: *gmax = max(0.0, max over the R regrets) as
  * fast_algorithms.py:228, :242-243 (bit-identical to the max of ocx_gT_regrets' output);
  * only 8 bytes leave the GPU.  What empirical_worst_case_thresholds needs per T. */
 int ocx_gT_max(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
                int lanes_per_seq, int device, double* gmax);
 /* In the bit-exact modes (lanes_per_seq 1 or -k) the comparator pass is the reference's
- * sequential sum; in the others the clipped-row closed form of ocx_dev_simulate_alg_ex
- * applies (the sampler's rows satisfy it by construction). */
+ * sequential sum; in the others the closed form of ocx_dev_simulate_alg_ex applies where
+ * the kernel certifies it (the sampler's rows satisfy it by construction). */
 
 /* fast_algorithms.py:211-247 empirical_worst_case_thresholds with `d` coordinates, over
  * several GPUs of this process: for every T of T_grid [nT], the runs [0, runs) are split
@@ -239,16 +263,19 @@ int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const doubl
                          double* cum_loss, double* comp_loss, double* x_last, void* stream);
 
 /* ocx_dev_simulate_alg with options.  flags (bitwise or):
- *   OCX_ALG_CLIPPED_ROWS  the caller asserts ||z_t|| <= 1 for every row (up to rounding),
- *     as the g(T) sampler's clipped rows (fast_algorithms.py:234-237, ocx_dev_gen_gT) are.
- *     With comparator == NULL, the loss of FTL(theta_T) over the sequence is then
- *     T/2 - ||theta_T|| whenever every step's sub-gradient was -y_t/2 (y_t = +-1, no exact
- *     tie; the kernel checks this per sequence), because |z_t.x* - y_t| = 1 - y_t z_t.x*
- *     on the unit ball and theta_T = -S_T/2.  A wave whose sequences all pass skips the
- *     second pass over z: one HBM pass instead of two.  The comparator loss then equals
- *     the reference's sequential sum up to that sum's rounding (about 1e-12 relative on
- *     the regret at T = 1e4; the loop itself keeps the layout's summation order); a
- *     sequence failing the check gets the streamed second pass, bit-identical to flags 0.
+ *   OCX_ALG_CLIPPED_ROWS (or its synonym OCX_ALG_CLOSED_COMPARATOR)  closed-form comparator
+ *     loss where the kernel certifies it.  With comparator == NULL, the loss of
+ *     FTL(theta_T) over the sequence is T/2 - ||theta_T|| whenever every row is inside the
+ *     unit ball (||z_t||^2 <= 1 + 1e-12, as the g(T) sampler's clipped rows are,
+ *     fast_algorithms.py:234-237) and every step's sub-gradient was -y_t/2 (y_t = +-1, no
+ *     exact tie), because |z_t.x* - y_t| = 1 - y_t z_t.x* on the unit ball and
+ *     theta_T = -S_T/2.  The kernel checks BOTH conditions itself, row by row and step by
+ *     step, for every sequence: the flag is a request, never a trusted assertion, and is
+ *     safe on any data.  A wave whose sequences all pass skips the second pass over z: one
+ *     HBM pass instead of two.  The comparator loss then equals the reference's sequential
+ *     sum up to that sum's rounding (about 1e-12 relative on the regret at T = 1e4; the
+ *     loop itself keeps the layout's summation order); a sequence failing the check gets
+ *     the streamed second pass, bit-identical to flags 0.
  * closed_out [B] (int32, nullable): 1 where the closed form was taken. */
 #define OCX_ALG_CLIPPED_ROWS 1
 int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,

@@ -61,11 +61,16 @@ SIGNATURES = {
                                            c_vp]),
     "ocx_ftrl_vs_exact_batch": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_double, c_dp, c_dp,
                                         c_dp, c_dp, c_dp, ctypes.POINTER(ctypes.c_int32), c_int,
-                                        c_int, c_int]),
+                                        c_int]),
+    "ocx_ftrl_vs_exact_batch_ex": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_double, c_dp, c_dp,
+                                           c_dp, c_dp, c_dp, ctypes.POINTER(ctypes.c_int32),
+                                           c_int, c_int, c_int]),
     "ocx_dev_ftrl_vs_exact": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_replay_batch": (c_int, [c_dp, c_dp, c_dp, c_i64, c_i64, c_i64, c_dp, c_dp, c_int]),
     "ocx_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp, c_int, c_int]),
+    "ocx_gT_regrets_dev": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_vp, c_int,
+                                   c_int]),
     "ocx_gT_max": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_int, c_int, c_dp]),
     "ocx_dev_pack": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_dev_gen_gT": (c_int, [ctypes.POINTER(Layout), c_u64, c_i64, c_vp, c_vp, c_vp]),
@@ -92,6 +97,13 @@ SIGNATURES = {
                                c_vp, c_vp, c_vp, c_vp]),
     "ocx_twin32_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_fp, c_int]),
 }
+# include/ocx_testing.h: test-only entry points (bound like the others, never called by the
+# package itself)
+TEST_SIGNATURES = {
+    "ocx_test_gT_regrets_unclean": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp,
+                                            c_int, c_int, c_i64]),
+}
+OCX_VERSION = 200  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1
 OCX_ALG_CLOSED_COMPARATOR = 2
 OCX_ALG_TREE_SUMS = 4
@@ -129,10 +141,13 @@ def load():
                 raise OCXError(f"libocx.so not found at {LIB_PATH}: the HIP extension is not "
                                "built (python -m online_convex_optimization_amd._build)")
             lib = ctypes.CDLL(LIB_PATH)
-            for name, (res, args) in SIGNATURES.items():
+            for name, (res, args) in {**SIGNATURES, **TEST_SIGNATURES}.items():
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            if lib.ocx_version() != OCX_VERSION:
+                raise OCXError(f"{LIB_PATH} implements ABI version {lib.ocx_version()}, this "
+                               f"binding expects {OCX_VERSION}: rebuild the library")
             _lib = lib
     return _lib
 

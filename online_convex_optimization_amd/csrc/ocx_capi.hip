@@ -14,9 +14,9 @@
 #include <vector>
 
 #include "../../include/ocx.h"
+#include "../../include/ocx_testing.h"
 #include "ocx_sim_kernels.h"
 
-#define OCX_VERSION 100  // 0.1.0
 
 namespace {
 
@@ -325,10 +325,12 @@ int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const do
                             int32_t* closed_out, void* stream) {
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
-    if (flags & ~OCX_ALG_CLIPPED_ROWS) return fail(OCX_E_INVALID, "unknown flags");
+    if (flags & ~(OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR))
+        return fail(OCX_E_INVALID, "unknown flags");
+    // the two flags are one request: the kernel certifies every row and sub-gradient itself
     OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag != 0 ? 1 : 0, eta0, comparator, regret,
                            cum_loss, comp_loss, x_last, (hipStream_t)stream, nullptr, closed_out,
-                           (flags & OCX_ALG_CLIPPED_ROWS) ? 1 : 0));
+                           (flags & (OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR)) ? 1 : 0));
     return OCX_OK;
 }
 
@@ -572,8 +574,16 @@ int ocx_ftl_prefix_actions_batch(const double* z, const double* y, int64_t B, in
 
 int ocx_ftrl_vs_exact_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                             double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
-                            double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
+                            double* comp_ftl, double* cmp_action, int32_t* regime,
                             int lanes_per_seq, int device) {
+    return ocx_ftrl_vs_exact_batch_ex(z, y, B, T, d, eta0, cum_ftrl, cum_exact, comp_exact,
+                                      comp_ftl, cmp_action, regime, 0, lanes_per_seq, device);
+}
+
+int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                               double eta0, double* cum_ftrl, double* cum_exact,
+                               double* comp_exact, double* comp_ftl, double* cmp_action,
+                               int32_t* regime, int norm, int lanes_per_seq, int device) {
     ocx_layout L;
     if (int rc = ocx_layout_init(B, T, d, lanes_per_seq, &L)) return rc;
     if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
@@ -660,8 +670,13 @@ namespace {
 
 // fast_algorithms.py:230-243 for one T: the regrets of runs [run0, run0 + R) to the host
 // (`regrets`), or only their max (`gmax`: the regrets never leave the GPU).
+// test_unclean_every (ocx_test_gT_regrets_unclean only, 0 elsewhere): on the streamed path,
+// mark every k-th run as failing the closed form's check, so the fallback pass is exercised.
+// regrets_on_device: `regrets` is device memory of `device` (ocx_gT_regrets_dev): the FTRL
+// kernel writes each batch's regrets straight into it and nothing crosses PCIe.
 int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
-           double* regrets, double* gmax, int lanes_per_seq, int device) {
+           double* regrets, double* gmax, int lanes_per_seq, int device,
+           int64_t test_unclean_every = 0, bool regrets_on_device = false) {
     if (R < 0 || run0 < 0 || T < 0 || d < 0) return fail(OCX_E_INVALID, "negative argument");
     if (gmax) *gmax = 0.0;
     if (R == 0) return OCX_OK;
@@ -679,12 +694,11 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         dmax = cx->gmax.as<unsigned long long>();
         OCX_HIP(hipMemsetAsync(dmax, 0, 8, st));  // +0.0
     }
-    // the max leaves the GPU once, after the last batch
+    // the max leaves the GPU once, after the last batch; device-resident regrets are
+    // complete when the call returns (any stream may read them then)
     auto finish = [&]() -> int {
-        if (dmax) {
-            OCX_HIP(hipMemcpyAsync(gmax, dmax, 8, hipMemcpyDeviceToHost, st));
-            OCX_HIP(hipStreamSynchronize(st));
-        }
+        if (dmax) OCX_HIP(hipMemcpyAsync(gmax, dmax, 8, hipMemcpyDeviceToHost, st));
+        if (dmax || regrets_on_device) OCX_HIP(hipStreamSynchronize(st));
         return OCX_OK;
     };
     // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB): by default 90 % of
@@ -770,12 +784,13 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
             OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
                                       cx->yt.as<double>(), st));
+            double* rdst = regrets_on_device ? regrets + r0 : cx->out.as<double>();
             OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
-                                   cx->out.as<double>(), nullptr, nullptr, nullptr, st, nullptr,
-                                   nullptr, onepass));
+                                   rdst, nullptr, nullptr, nullptr, st, nullptr, nullptr,
+                                   onepass));
             if (dmax) {
                 OCX_HIP(launch_max_fold(cx->out.as<double>(), nb, dmax, st));
-            } else {
+            } else if (!regrets_on_device) {
                 OCX_HIP(hipMemcpyAsync(regrets + r0, cx->out.p, (size_t)nb * 8,
                                        hipMemcpyDeviceToHost, st));
                 OCX_HIP(hipStreamSynchronize(st));
@@ -798,8 +813,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
     if (int rc = ocx_layout_init(R % Bc ? R % Bc : Bc, 1, d, lanes_per_seq, &Ltail)) return rc;
     OCX_HIP(cx->theta.ensure((size_t)std::max(Bc * L1.Dp, Ltail.B * Ltail.Dp) * 8));
     OCX_HIP(cx->acc.ensure((size_t)(Bc * 4 + 1) * 8));
-    int64_t unclean_every = 0;
-    if (const char* e = std::getenv("OCX_TEST_UNCLEAN_EVERY")) unclean_every = std::atoll(e);
+    const int64_t unclean_every = test_unclean_every;
     for (int64_t r0 = 0; r0 < R; r0 += Bc) {
         const int64_t nb = std::min(Bc, R - r0);
         ocx_layout Lb;
@@ -816,7 +830,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         OCX_HIP(hipMemsetAsync(cum, 0, (size_t)Bc * 2 * 8, st));
         if (unclean) OCX_HIP(hipMemsetAsync(unclean, 0, (size_t)(nb + 1) * 8, st));
         if (unclean && unclean_every > 0) {
-            // test knob (OCX_TEST_UNCLEAN_EVERY=k): mark runs r0 + b with b % k == 0 as if a
+            // test hook (ocx_test_gT_regrets_unclean, k): mark runs r0 + b with b % k == 0 as if a
             // step had failed the closed form's check, so the second pass serves them
             std::vector<double> mk((size_t)nb, 0.0);
             for (int64_t i = 0; i < nb; i += unclean_every) mk[(size_t)i] = 1.0;
@@ -853,6 +867,8 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         }
         if (dmax) {
             OCX_HIP(launch_max_fold(reg, nb, dmax, st));
+        } else if (regrets_on_device) {
+            OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToDevice, st));
         } else {
             OCX_HIP(hipMemcpyAsync(regrets + r0, reg, (size_t)nb * 8, hipMemcpyDeviceToHost, st));
             OCX_HIP(hipStreamSynchronize(st));
@@ -869,6 +885,22 @@ int ocx_gT_regrets(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64
                    double eta0, double* regrets, int lanes_per_seq, int device) {
     if (!regrets && R > 0) return fail(OCX_E_INVALID, "NULL regrets");
     return gT_run(base_seed, T, run0, R, d, eta0, regrets, nullptr, lanes_per_seq, device);
+}
+
+int ocx_gT_regrets_dev(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d,
+                       double eta0, double* regrets_dev, int lanes_per_seq, int device) {
+    if (!regrets_dev && R > 0) return fail(OCX_E_INVALID, "NULL regrets");
+    return gT_run(base_seed, T, run0, R, d, eta0, regrets_dev, nullptr, lanes_per_seq, device, 0,
+                  true);
+}
+
+int ocx_test_gT_regrets_unclean(uint64_t base_seed, int64_t T, int64_t run0, int64_t R,
+                                int64_t d, double eta0, double* regrets, int lanes_per_seq,
+                                int device, int64_t unclean_every) {
+    if (!regrets && R > 0) return fail(OCX_E_INVALID, "NULL regrets");
+    if (unclean_every < 1) return fail(OCX_E_INVALID, "unclean_every must be >= 1");
+    return gT_run(base_seed, T, run0, R, d, eta0, regrets, nullptr, lanes_per_seq, device,
+                  unclean_every);
 }
 
 int ocx_gT_max(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,

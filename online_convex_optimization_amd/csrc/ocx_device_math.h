@@ -324,6 +324,20 @@ __device__ __forceinline__ void ocx_action_exact_poly(const double (&th)[C], dou
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ bool ocx_dual_ok(const ocx_d2* z, int norm, int lane);
 
+// Certification test of the closed-form comparators (ocx_alg_kernel onepass,
+// ocx_alg_chunk_kernel): is ||z_t||_2^2 <= 1 + 1e-12 for this row?  Not part of the
+// reference's arithmetic, so any summation order does (fused lane sums, butterfly); the
+// 1e-12 slack admits rows clipped in floating point (np.linalg.norm ∘ z / max(n, 1)
+// leaves ||z_t|| within a few ulps of 1).  Every lane of the sequence gets the answer; call
+// it with the whole wave active (the butterfly reads neighbouring lanes).
+template <int C, int P>
+__device__ __forceinline__ bool ocx_row_in_ball(const ocx_d2* z) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < C; ++j) acc = __builtin_fma(ocx_zj(z, j), ocx_zj(z, j), acc);
+    return ocx_seq_sum<P>(acc) <= 1.0 + 1e-12;
+}
+
 template <int C, int P, bool CHAIN>
 __device__ __forceinline__ double ocx_zdot(const ocx_d2* z, const double (&x)[C], int lane) {
     double p[C];

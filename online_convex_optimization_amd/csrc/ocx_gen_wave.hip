@@ -20,7 +20,9 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <utility>
 
 #include "ocx_internal.h"
 #include "ocx_rng.h"
@@ -824,18 +826,22 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
         if (n > 0 && n < cus) cus = n;
     }
     {
-        // the occupancy of an instance depends only on its LDS size here: query once
+        // the occupancy of this instance on a device depends only on its LDS size: query
+        // once per (device, LDS size) — a device list may mix GPUs, and host threads of
+        // ocx_gT_sweep_devices launch concurrently
         static std::mutex mu;
-        static size_t q_lds = ~(size_t)0;
-        static int q_per_cu = 0;
+        static std::map<std::pair<int, size_t>, int> cache;
         std::lock_guard<std::mutex> lk(mu);
-        if (q_lds != lds) {
+        const auto key = std::make_pair(dev, lds);
+        auto it = cache.find(key);
+        if (it == cache.end()) {
+            int q = 0;
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &q_per_cu, ocx_gen_wave_kernel<MODE, DF, LR, RAW>, kWaveBlock, lds);
+                &q, ocx_gen_wave_kernel<MODE, DF, LR, RAW>, kWaveBlock, lds);
             if (e != hipSuccess) return e;
-            q_lds = lds;
+            it = cache.emplace(key, q).first;
         }
-        per_cu = q_per_cu;
+        per_cu = it->second;
     }
     int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
     // OCX_GEN_WAVES_PER_SIMD caps the resident generator waves (leaves registers free for

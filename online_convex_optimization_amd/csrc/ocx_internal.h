@@ -23,12 +23,13 @@ __device__ __forceinline__ int64_t ocx_wave_id() {
 // then lands on G/4 CUs and leaves the rest idle: below 8 waves per CU use one-wave
 // blocks, which the dispatcher spreads over every CU.  OCX_BLOCK_WAVES=1|2|4 forces it.
 inline int ocx_block_waves(int64_t G) {
-    static int forced = -1;
-    if (forced < 0) {
+    // read once, thread-safe (host threads of ocx_gT_sweep_devices launch concurrently):
+    // a function-local static's initialiser runs exactly once (C++11 magic statics)
+    static const int forced = [] {
         const char* e = std::getenv("OCX_BLOCK_WAVES");
         const int v = e ? std::atoi(e) : 0;
-        forced = (v == 1 || v == 2 || v == 4) ? v : 0;
-    }
+        return (v == 1 || v == 2 || v == 4) ? v : 0;
+    }();
     if (forced) return forced;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -127,6 +127,9 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 const double diff = q - yb[u];  // :106-111
                 cum += 0.5 * fabs(diff);
                 double gq = ocx_grad(diff);
+                // the closed form needs ||z_t|| <= 1 too: certified here, row by row,
+                // whatever the caller asserts (whole wave active: the test sums across lanes)
+                if (onepass) clean = clean & ocx_row_in_ball<C, P>(zb[u]);
                 clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
                 if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
                     linear = linear && ocx_dual_ok<C, P, CHAIN>(zb[u], norm, lane) &&
@@ -140,8 +143,8 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     }
 
     // ---- closed-form comparator (onepass) ----
-    // For rows with ||z_t|| <= 1 (the g(T) sampler's clipped rows: the caller asserts it)
-    // and x* = FTL(theta_T) in the unit ball, |z_t.x* − y_t| = 1 − y_t z_t.x* when y_t = ±1,
+    // For rows with ||z_t|| <= 1 (the g(T) sampler's clipped rows; certified per row in
+    // the loop above, ocx_row_in_ball) and x* = FTL(theta_T) in the unit ball, |z_t.x* − y_t| = 1 − y_t z_t.x* when y_t = ±1,
     // so the comparator loss is ½(T − x*.S_T), S_T = Σ y_t z_t.  If every step's
     // sub-gradient was −y_t/2 (no tie, y_t = ±1: `clean`), theta_T = −½ S_T exactly
     // (powers of two), x* = −theta/||theta|| and the loss is T/2 − ||theta_T||: no second

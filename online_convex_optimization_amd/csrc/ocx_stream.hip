@@ -14,7 +14,8 @@
 #include "ocx_sim_kernels.h"
 
 // mode 0: loop steps [t0, t0+Tc) of fast_algorithms.py:99-111, theta/cum in & out;
-//         unclean[b] (nullable) is set to 1 when a step's sub-gradient is not −y_t/2.
+//         unclean[b] (nullable) is set to 1 when a step's sub-gradient is not −y_t/2
+//         or its row is not inside the unit ball (ocx_row_in_ball).
 // mode 1: comparator loss of those steps with x* = FTL(theta_state); when regret_out
 //         is non-null (last chunk) also regret = cum - comp (only where unclean[b] != 0
 //         when unclean is given: the clean sequences took the closed form in mode 2).
@@ -106,6 +107,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_chunk_kernel(
                     const double diff = q - yb[u];
                     cum += 0.5 * fabs(diff);
                     const double gq = ocx_grad(diff);
+                    // closed form: rows certified inside the unit ball (ocx_row_in_ball)
+                    if (unclean != nullptr) clean = clean & ocx_row_in_ball<C, P>(zb[u]);
                     clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
 #pragma unroll
                     for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);

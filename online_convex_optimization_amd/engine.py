@@ -11,13 +11,16 @@ Two ways in:
   from PyTorch (plumbing only); every kernel is the HIP code in ``csrc/``.
 
 Every batched call defaults to ``lanes_per_seq=LANES_BEST`` (include/ocx.h,
-OCX_LANES_BEST): the exact layout — the reference's sequential sums, bit-identical
-results — wherever its lane chains are short and the kernels stream at the HBM roofline
-(e.g. d=64 with >= 8192 sequences per batch, every d <= 16 batch), and butterfly sums
-(~1e-16 relative) where an exact chain of 8+ lanes would leave the kernel latency-bound:
-d >= 512 and few-wave batches (the capacity-limited T=1e5 g(T) batch).
-``lanes_per_seq=1`` forces the bit-exact layout; the drop-in modules (fast_algorithms,
-exact_ftl) always use it.
+OCX_LANES_BEST), the fastest certified mode: the exact layout's sequential sums wherever its
+lane chains are short and the kernels stream at the HBM roofline (e.g. d=64 with >= 8192
+sequences per batch, every d <= 16 batch), butterfly sums (~1e-16 relative) where an exact
+chain of 8+ lanes would leave the kernel latency-bound (d >= 512, few-wave batches such as
+the capacity-limited T=1e5 g(T) batch), and — for the g(T), DeviceBatch and FTRL-vs-exact
+paths — the closed-form comparator losses wherever the kernel certifies them (one HBM pass
+instead of two; about 1e-13 relative on the regret).  LANES_BEST results are therefore NOT
+bit-identical to the reference.  ``lanes_per_seq=1`` forces the bit-exact mode (sequential
+sums, streamed comparator pass); the drop-in modules (fast_algorithms, exact_ftl) always use
+it.
 """
 from __future__ import annotations
 
@@ -186,7 +189,7 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, norm: str = "l2",
     cr, ce, cmp_e, cmp_f = (np.zeros(B) for _ in range(4))
     act = np.zeros((B, d))
     rg = np.zeros(B, dtype=np.int32)
-    _lib.call("ocx_ftrl_vs_exact_batch", ptr(z), ptr(y), B, T, d, float(eta0), ptr(cr), ptr(ce),
+    _lib.call("ocx_ftrl_vs_exact_batch_ex", ptr(z), ptr(y), B, T, d, float(eta0), ptr(cr), ptr(ce),
               ptr(cmp_e), ptr(cmp_f) if with_ftl_comparator else None, ptr(act),
               rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _norm_code(norm),
               int(lanes_per_seq), int(device))
@@ -209,6 +212,29 @@ def gT_regrets(T: int, runs: int, *, base_seed: int = 0, d: int = 5, eta0: float
     out = np.zeros(int(runs))
     _lib.call("ocx_gT_regrets", int(base_seed), int(T), int(run0), int(runs), int(d),
               float(eta0), ptr(out), int(lanes_per_seq), int(device))
+    return out
+
+
+def gT_regrets_device(T: int, runs: int, *, base_seed: int = 0, d: int = 5,
+                      eta0: float = SQRT2, run0: int = 0, lanes_per_seq: int = LANES_BEST,
+                      device: int = 0, out=None):
+    """gT_regrets with the regrets left in HBM (``ocx_gT_regrets_dev``): a float64 torch
+    tensor [runs] on cuda:``device`` (``out`` if given), complete when this returns.  What a
+    rank hands to an RCCL all-gather (parallel.gT_sweep_distributed): no host round trip."""
+    import torch
+    if base_seed < 0 or base_seed >= 2 ** 64:
+        raise ValueError("base_seed must be in [0, 2**64)")
+    dev = torch.device("cuda", int(device))
+    if out is None:
+        out = torch.empty(int(runs), dtype=torch.float64, device=dev)
+    if out.dtype != torch.float64 or out.device != dev or not out.is_contiguous() \
+            or out.numel() != int(runs):
+        raise ValueError(f"out must be a contiguous float64 tensor of {runs} on {dev}")
+    # the library writes on its own stream: let the allocating stream's pending work on
+    # this memory finish first
+    torch.cuda.current_stream(dev).synchronize()
+    _lib.call("ocx_gT_regrets_dev", int(base_seed), int(T), int(run0), int(runs), int(d),
+              float(eta0), ctypes.c_void_p(out.data_ptr()), int(lanes_per_seq), int(device))
     return out
 
 
@@ -415,18 +441,19 @@ class DeviceBatch:
                      x_last=None, closed_comparator: Optional[bool] = None, closed_out=None):
         """Launch the FTRL/FTL kernel; results land in self.regret/cum/comp (async).
 
-        ``closed_comparator`` (default: the batch holds g(T)-sampler rows, which are
-        clipped to ||z_t|| <= 1, and its layout is not a bit-exact mode) takes the
-        comparator loss in closed form, T/2 - ||theta_T||, wherever the kernel can certify
-        it, and so reads z once instead of twice (ocx_dev_simulate_alg_ex,
-        OCX_ALG_CLIPPED_ROWS); the regret then equals the reference's up to rounding.
-        Passing True for packed data asserts that its rows satisfy ||z_t|| <= 1.
+        ``closed_comparator`` (default: the layout is not a bit-exact mode) takes the
+        comparator loss in closed form, T/2 - ||theta_T||, wherever the kernel certifies
+        it — every row inside the unit ball, every sub-gradient -y_t/2, checked on device
+        per sequence — and so reads z once instead of twice (ocx_dev_simulate_alg_ex,
+        OCX_ALG_CLIPPED_ROWS); the regret then equals the reference's up to rounding.  It is
+        safe on any data: sequences that fail the check stream the second pass and are
+        bit-identical to ``closed_comparator=False``.
         ``closed_out`` ([B] int32 device tensor, optional) receives 1 per sequence that took
         the closed form, 0 where the kernel streamed the second pass."""
         cp = comparator.data_ptr() if comparator is not None else None
         xp = x_last.data_ptr() if x_last is not None else None
         if closed_comparator is None:
-            closed_comparator = self.rows_clipped and not self.exact and comparator is None
+            closed_comparator = not self.exact and comparator is None
         flags = _lib.OCX_ALG_CLIPPED_ROWS if closed_comparator else 0
         _lib.call("ocx_dev_simulate_alg_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   int(alg_flag), float(eta0), cp, self.regret.data_ptr(), self.cum.data_ptr(),

@@ -13,27 +13,32 @@ from tests._tiles import untile_y, untile_z
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    with open(os.path.join(ROOT, "include", "ocx.h")) as f:
+def declared_symbols(header="ocx.h"):
+    with open(os.path.join(ROOT, "include", header)) as f:
         txt = f.read()
     return sorted(set(re.findall(r"^\s*int\s+(ocx_\w+)\s*\(", txt, flags=re.M)))
 
 
-def test_library_exports_every_declared_symbol():
+@pytest.mark.parametrize("header,table", [("ocx.h", "SIGNATURES"),
+                                          ("ocx_testing.h", "TEST_SIGNATURES")])
+def test_library_exports_every_declared_symbol(header, table):
     lib = _lib.load()
-    syms = declared_symbols()
-    assert len(syms) >= 14
+    syms = declared_symbols(header)
+    assert len(syms) >= (14 if header == "ocx.h" else 1)
     for s in syms:
         assert hasattr(lib, s), s
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True,
                          text=True, check=True).stdout
     exported = set(re.findall(r" T (ocx_\w+)$", out, flags=re.M))
     assert set(syms) <= exported
-    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+    sig = getattr(_lib, table)
+    assert set(syms) == set(sig), set(syms) ^ set(sig)
 
 
 def test_version_and_error_channel():
-    assert _lib.load().ocx_version() == 100
+    with open(os.path.join(ROOT, "include", "ocx.h")) as f:
+        ver = int(re.search(r"#define OCX_VERSION (\d+)", f.read()).group(1))
+    assert _lib.load().ocx_version() == ver == _lib.OCX_VERSION == 200
     with pytest.raises(ValueError):
         _lib.layout(-1, 10, 5)
     assert "negative" in _lib.last_error()

@@ -34,7 +34,12 @@ def _worker(rank, world, port, T_grid, runs, q):
         return np.array([O.simulate_alg(*O.gT_sample(0, T, r, 5), 0, math.sqrt(2))
                          for r in range(run0, run0 + count)])
     res = gT_sweep_distributed(T_grid, runs, compute=compute)
-    q.put((rank, {T: (g, regs.tolist()) for T, (g, regs) in res.items()}))
+    # g(T) alone: each rank's shard max, one all_reduce(MAX) of one double per T
+    gonly = gT_sweep_distributed(T_grid, runs, compute=compute,
+                                 compute_max=lambda T, r0, n: max(0.0, float(np.max(
+                                     compute(T, r0, n), initial=0.0))),
+                                 return_regrets=False)
+    q.put((rank, {T: (g, regs.tolist(), gonly[T]) for T, (g, regs) in res.items()}))
     dist.destroy_process_group()
 
 
@@ -72,7 +77,7 @@ def test_gT_sweep_world2_matches_single_process(world):
     ref = O.empirical_worst_case_thresholds(T_grid, runs=runs)
     for rank in range(world):
         for T in T_grid:
-            g, regs = results[rank][T]
-            assert g == ref[T]
+            g, regs, (g_only, none) = results[rank][T]
+            assert g == ref[T] and g_only == ref[T] and none is None
             assert len(regs) == runs
             assert regs == results[0][T][1]

@@ -1,0 +1,103 @@
+"""GPU tests at BASELINE.json's full configuration sizes that the per-kernel parity tests do
+not reach:
+
+* configs[3] at its longest horizon, T = 1e5 (d = 64): one resident g(T) batch of the size
+  the sweep really runs (about 4 900 sequences: the HBM budget caps it), on the default
+  path (OCX_LANES_BEST's butterfly 8 x 8 layout + the certified closed-form comparator),
+  against the bit-exact mode and the oracle (fast_algorithms.py:211-247);
+* configs[2]'s exact side at T = 1e4 (d = 64): FTRL against exact FTL in one kernel
+  (ocx_ftrl_vs_exact_kernel) on the default path and in the bit-exact mode, against the
+  oracle's closed form (exact_ftl_driver.py:157-186, exact_ftl.py:280-333, :399-420).
+
+Bars as tests/test_gpu_parity.py: bit-exact in exact mode, close_closed for the default."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.test_gpu_parity import close, close_closed
+
+pytestmark = pytest.mark.gpu
+
+SQ2 = math.sqrt(2)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from online_convex_optimization_amd import _lib, engine
+    assert _lib.device_count() >= 1
+    return engine
+
+
+def _free_device_memory(eng):
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    eng.release_buffers()
+
+
+def test_config3_T1e5_resident_batch(eng):
+    """configs[3], T = 1e5, d = 64: the sweep's resident batch (4 900 runs, ≈255 GB of
+    tiles) on the default path vs exact mode and the oracle; g(T) reduced on device."""
+    from online_convex_optimization_amd import _lib
+    T, d, runs = 100000, 64, 4900
+    L = _lib.layout(runs, T, d, eng.LANES_BEST)
+    assert (L.P, L.C, L.chain) == (8, 8, 0)        # the BEST butterfly shape of this batch
+    _free_device_memory(eng)
+    try:
+        reg = eng.gT_regrets(T, runs, base_seed=0, d=d)            # default: BEST + closed
+        gmax = eng.gT_max(T, runs, base_seed=0, d=d)
+        ex = eng.gT_regrets(T, runs, base_seed=0, d=d, lanes_per_seq=1)  # bit-exact mode
+    finally:
+        eng.release_buffers()
+    assert np.all(np.isfinite(reg)) and np.all(np.isfinite(ex))
+    assert close_closed(reg, ex, T)
+    assert gmax == eng.max_regret(reg)
+    for r in (0, 1, runs // 2, runs - 1):
+        z, y = O.gT_sample(0, T, r, d)
+        ref = O.simulate_alg(z, y, 0, SQ2)
+        assert ex[r] == ref, (r, ex[r], ref)
+        assert close_closed(reg[r], ref, T), (r, reg[r], ref)
+
+
+def test_config2_exact_side_T1e4(eng):
+    """configs[2]'s exact side, d = 64, T = 1e4: FTRL vs exact FTL (l2 ball) per sequence in
+    one kernel.  Default (closed-form comparators, butterfly sums) vs exact mode (two
+    passes, sequential sums) on 2 048 device-generated sequences; sampled sequences vs the
+    oracle's exact-FTL closed form and its FTRL run against that comparator."""
+    import torch
+    B, T, d = 2048, 10000, 64
+    _free_device_memory(eng)
+    outs = {}
+    for name, lanes in (("best", eng.LANES_BEST), ("exact", 1)):
+        db = eng.DeviceBatch(B, T, d, lanes_per_seq=lanes).generate_gT(base_seed=3)
+        cf = torch.zeros(B, dtype=torch.float64, device=db.device)
+        act = torch.zeros((B, d), dtype=torch.float64, device=db.device)
+        rg = db.ftrl_vs_exact(SQ2, comp_ftl=cf, cmp_action=act)
+        torch.cuda.synchronize()
+        outs[name] = {"cum": db.cum.cpu().numpy(), "cum_exact": db.cum_exact.cpu().numpy(),
+                      "comp": db.comp.cpu().numpy(), "comp_ftl": cf.cpu().numpy(),
+                      "action": act.cpu().numpy(), "regime": rg.cpu().numpy()}
+        del db, cf, act, rg
+        _free_device_memory(eng)
+    bst, ext = outs["best"], outs["exact"]
+    assert np.all(bst["regime"] == 1) and np.all(ext["regime"] == 1)
+    for k in ("cum", "cum_exact"):   # the loops: butterfly vs sequential sums
+        assert close(bst[k], ext[k]), k
+    for k in ("comp", "comp_ftl"):   # closed form vs the streamed sums
+        assert close_closed(bst[k], ext[k], T), k
+    assert close(bst["action"], ext["action"])
+    ftrl_b, ftrl_e = bst["cum"] - bst["comp"], ext["cum"] - ext["comp"]
+    assert close_closed(ftrl_b, ftrl_e, T)
+    for b in (0, 1, B // 2, B - 1):
+        z, y = O.gT_sample(3, T, b, d)
+        rc, rp, ra, ok = O.ftl_exact_closed_form(z, y)
+        assert ok
+        fr = O.simulate_alg_full(z, y, 0, SQ2, comparator=ra)
+        ff = O.simulate_alg_full(z, y, 0, SQ2)
+        got = [ext["cum_exact"][b], ext["comp"][b], ext["cum"][b], ext["comp_ftl"][b]]
+        assert got == [rc, rp, fr[1], ff[2]], b
+        assert np.array_equal(ext["action"][b], ra), b
+        assert close_closed([bst["cum_exact"][b] - bst["comp"][b], ftrl_b[b]],
+                            [rc - rp, fr[0]], T), b

@@ -1,7 +1,8 @@
 """GPU: the product's multi-device code paths on a one-GPU box.
 
-* parallel.gT_sweep_distributed with its DEFAULT compute (engine.gT_regrets on the rank's
-  GPU), world_size 2 over gloo, both ranks on device 0, ragged shards;
+* parallel.gT_sweep_distributed with its DEFAULT compute (device-resident regrets from
+  engine.gT_regrets_device on the rank's GPU, or ocx_gT_max + one all_reduce(MAX) for g(T)
+  alone), world_size 2 over gloo, both ranks on device 0, ragged shards;
 * the same over the "nccl" backend (RCCL) with world_size 1: RCCL initialisation and the
   device all-gather run for real (two ranks cannot share one GPU under RCCL);
 * engine.gT_sweep(devices=[0, 0]): one process driving a device list from threads.
@@ -46,7 +47,17 @@ def _worker(rank, world, port, backend, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = gT_sweep_distributed(T_GRID, RUNS, base_seed=3, d=D)
-        q.put((rank, {T: (g, regs.tolist()) for T, (g, regs) in res.items()}))
+        # regret curves gathered device to device, kept as tensors
+        tens = gT_sweep_distributed(T_GRID, RUNS, base_seed=3, d=D, as_tensor=True)
+        dev_ok = all(isinstance(v, torch.Tensor) and v.dtype == torch.float64 and
+                     v.device.type == ("cuda" if backend == "nccl" else "cpu")
+                     for _, v in tens.values())
+        same = all(np.array_equal(tens[T][1].cpu().numpy(), res[T][1]) and
+                   tens[T][0] == res[T][0] for T in T_GRID)
+        # g(T) alone: ocx_gT_max per rank + one all_reduce(MAX)
+        gonly = gT_sweep_distributed(T_GRID, RUNS, base_seed=3, d=D, return_regrets=False)
+        q.put((rank, {T: (g, regs.tolist(), gonly[T][0], gonly[T][1] is None, dev_ok and same)
+                      for T, (g, regs) in res.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -87,9 +98,10 @@ def test_gT_sweep_distributed_default_compute(reference, world, backend):
     results = _run(world, backend)
     for rank in range(world):
         for T in T_GRID:
-            g, regs = results[rank][T]
+            g, regs, g_only, none, tens_ok = results[rank][T]
             assert np.array_equal(np.array(regs), reference[T]), (backend, rank, T)
             assert g == max(0.0, float(reference[T].max()))
+            assert g_only == g and none and tens_ok, (backend, rank, T)
 
 
 def test_gT_sweep_device_list(reference):
@@ -123,3 +135,21 @@ def test_gT_max_on_device(reference):
     finally:
         del os.environ["OCX_HBM_BUDGET_GB"]
     assert engine.gT_max(T_GRID[0], 0, base_seed=3, d=D) == 0.0
+
+
+def test_gT_regrets_device(reference, monkeypatch):
+    """engine.gT_regrets_device (ocx_gT_regrets_dev): the regrets land in a device tensor,
+    bit-identical to the host-array entry point, on the resident and the streamed path."""
+    import torch
+    from online_convex_optimization_amd import engine
+    for T in T_GRID:
+        t = engine.gT_regrets_device(T, RUNS, base_seed=3, d=D)
+        assert t.is_cuda and np.array_equal(t.cpu().numpy(), reference[T])
+        sub = torch.full((RUNS - 5,), -7.0, dtype=torch.float64, device="cuda")
+        engine.gT_regrets_device(T, RUNS - 5, base_seed=3, d=D, run0=5, out=sub)
+        assert np.array_equal(sub.cpu().numpy(), reference[T][5:])
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", "0.0004")  # streamed path (T-chunks)
+    t = engine.gT_regrets_device(T_GRID[1], RUNS, base_seed=3, d=D)
+    assert np.array_equal(t.cpu().numpy(), reference[T_GRID[1]])
+    with pytest.raises(ValueError):
+        engine.gT_regrets_device(40, 3, out=torch.zeros(4, dtype=torch.float64, device="cuda"))

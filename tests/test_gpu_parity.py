@@ -394,9 +394,11 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
 @pytest.mark.parametrize("T,d,runs,exact", [(200, 64, 700, False), (60, 64, 9000, True),
                                              (40, 1024, 40, False), (300, 5, 500, True)])
 def test_best_mode_default(ocx, T, d, runs, exact):
-    """The batched APIs' default (OCX_LANES_BEST): the exact layout (bit-identical) where
-    its chains are short — d=64 with >= 8192 sequences, small d — and butterfly sums
-    (<= 1e-12 relative) for few-wave d=64 batches and d=1024."""
+    """The batched APIs' default (OCX_LANES_BEST): the exact layout's sums where its chains
+    are short — d=64 with >= 8192 sequences, small d — and butterfly sums for few-wave d=64
+    batches and d=1024, with the certified closed-form comparator in both cases, so the
+    default is held to close_closed against the oracle, never to bit equality (the
+    bit-exact mode, lanes_per_seq=1, is checked bit for bit beside it)."""
     eng, lib = ocx["engine"], ocx["lib"]
     L = lib.layout(runs, T, d, eng.LANES_BEST)
     assert bool(L.P == 1 or L.chain) == exact
@@ -575,8 +577,10 @@ def test_closed_comparator_matches_two_pass(ocx, B, T, d, P):
 @pytest.mark.parametrize("P", [-1, 128, 0])
 def test_closed_comparator_falls_back(ocx, P):
     """Sequences whose sub-gradients are not all -y_t/2 (a label of 0.5, a zero row with a
-    zero label: an exact tie) take the second pass, bit-identical to the two-pass kernel;
-    the clean sequences of the same waves keep the closed form."""
+    zero label: an exact tie) or with a row outside the unit ball (1.5x, and one just
+    outside, 1 + 1e-9: the kernel certifies ||z_t|| <= 1 itself, closed_comparator=True is
+    only a request) take the second pass, bit-identical to the two-pass kernel; the clean
+    sequences of the same waves keep the closed form."""
     import torch
     eng = ocx["engine"]
     rng = np.random.default_rng(3)
@@ -588,18 +592,28 @@ def test_closed_comparator_falls_back(ocx, P):
     z[9, 0] = 0.0
     y[9, 0] = 0.0                        # q - y == 0: the sub-gradient is 0, not -y/2
     y[40, T - 1] = 0.25
+    z[12, 30] *= 1.5 / np.linalg.norm(z[12, 30])            # a row far outside the ball
+    z[61, T - 1] *= (1.0 + 1e-9) / np.linalg.norm(z[61, T - 1])  # just outside it
+    unclean = {5, 9, 12, 40, 61}
     db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y)
     assert not db.rows_clipped
     two = db.simulate_alg(closed_comparator=False).clone()
     flag = torch.full((B,), 7, dtype=torch.int32, device=db.device)
     one = db.simulate_alg(closed_comparator=True, closed_out=flag).clone()
+    dflt = torch.full((B,), 7, dtype=torch.int32, device=db.device)
+    auto = db.simulate_alg(closed_out=dflt).clone()  # default: the closed form outside exact modes
     torch.cuda.synchronize()
     two, one, flag = two.cpu().numpy(), one.cpu().numpy(), flag.cpu().numpy()
-    assert set(np.nonzero(flag == 0)[0]) == {5, 9, 40} and np.all(flag[flag != 0] == 1)
-    for b in (5, 9, 40):
+    assert set(np.nonzero(flag == 0)[0]) == unclean and np.all(flag[flag != 0] == 1)
+    if db.exact:
+        assert np.array_equal(auto.cpu().numpy(), two)
+    else:
+        assert np.array_equal(auto.cpu().numpy(), one)
+        assert np.array_equal(dflt.cpu().numpy(), flag)
+    for b in unclean:
         assert one[b] == two[b], b
     assert close_closed(one, two, T)
-    for b in (0, 5, 9, 40, B - 1):
+    for b in (0, 5, 9, 12, 40, 61, B - 1):
         assert close_closed(one[b], O.simulate_alg(z[b], y[b], 0, SQ2), T), b
 
 
@@ -669,9 +683,10 @@ def test_ftrl_vs_exact_closed_form(ocx, P):
 @pytest.mark.parametrize("P", [0, 128])
 def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
     """The streamed path's closed form (ocx_alg_chunk_kernel mode 2) and its fallback: with
-    every third run marked as failing the check (OCX_TEST_UNCLEAN_EVERY, a test knob), those
-    runs get the regenerated second pass, bit-identical to the resident two-pass kernel; the
-    rest keep the closed form, bit-identical to the resident closed form."""
+    every third run marked as failing the check (ocx_test_gT_regrets_unclean, the test-only
+    entry point of include/ocx_testing.h), those runs get the regenerated second pass,
+    bit-identical to the resident two-pass kernel; the rest keep the closed form,
+    bit-identical to the resident closed form."""
     import torch
     eng = ocx["engine"]
     T, d, runs = 257, 64, 40
@@ -685,8 +700,9 @@ def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
     monkeypatch.setenv("OCX_MIN_RESIDENT", str(1 << 30))
     plain = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
     assert np.array_equal(plain, closed)
-    monkeypatch.setenv("OCX_TEST_UNCLEAN_EVERY", "3")
-    mixed = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
+    lib = ocx["lib"]
+    mixed = np.zeros(runs)
+    lib.call("ocx_test_gT_regrets_unclean", 4, T, 7, runs, d, SQ2, lib.ptr(mixed), P, 0, 3)
     marked = np.arange(runs) % 3 == 0
     assert np.array_equal(mixed[marked], two[marked])
     assert np.array_equal(mixed[~marked], closed[~marked])
