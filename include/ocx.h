@@ -111,7 +111,10 @@ int ocx_simulate_alg_batch(const double* z, const double* y, int64_t B, int64_t 
                            int lanes_per_seq, int device);
 
 /* fast_algorithms.py:184-195 simulate_SMART_like (→ :118-164), batched; thresh [B].
- * switch_step [B] nullable: the t at which the switch fired, or -1. */
+ * switch_step [B] nullable: the t at which the switch fired, or -1.  In the bit-exact modes
+ * (lanes_per_seq 1 or -k) the reference's O(T²·d) prefix re-scan and streamed comparator;
+ * otherwise the O(T·d) kernel of ocx_dev_simulate_smart_ex with both flags (the same
+ * switch steps; the comparator loss within its rounding). */
 int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                              const double* thresh, double eta0, double* regret,
                              int64_t* switch_step, int lanes_per_seq, int device);
@@ -322,6 +325,25 @@ int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const d
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                            const double* thresh, double eta0, double* regret,
                            int64_t* switch_step, void* stream);
+
+/* ocx_dev_simulate_smart with options.  flags (bitwise or):
+ *   OCX_SMART_CLOSED_PREFIX  O(T·d): the pre-switch prefix loss (:157-160) in closed form,
+ *     (t+1)/2 − ½ s_t·S_t with S_t = Σ_{i<=t} y_i z_i, valid while every row is in the unit
+ *     ball (||z_i||² <= 1 + 1e-12) and every label is ±1 (the kernel checks both).  It only
+ *     decides the switch where ftl_loss − s_loss is farther from the threshold than a bound
+ *     on the rounding that separates it from the reference's sequential sum; inside that
+ *     band, or outside the regime, the step re-scans its prefix as the reference does.  The
+ *     switch steps, hence the regrets, are the reference's.
+ *   OCX_ALG_CLOSED_COMPARATOR  the final comparator loss of FTL(theta_ftl) as T/2 −
+ *     ||theta_ftl|| where certified (as ocx_dev_simulate_alg_ex): one HBM pass in all, the
+ *     regret then within the comparator sum's rounding of the reference's.
+ * stats (nullable, device uint64 [2]): += steps that re-scanned, += sequences that took the
+ * closed comparator. */
+#define OCX_SMART_CLOSED_PREFIX 8
+int ocx_dev_simulate_smart_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                              const double* thresh, double eta0, double* regret,
+                              int64_t* switch_step, int flags, unsigned long long* stats,
+                              void* stream);
 
 /* exact_ftl.py:306-333 on device; a_tiled is the actions [B][T+1][d] tiled with a
  * layout of T+1 steps (z/y use L, actions use La with La->T == L->T + 1). */

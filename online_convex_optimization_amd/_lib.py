@@ -80,6 +80,8 @@ SIGNATURES = {
                                      c_vp, c_vp, c_vp, c_vp, c_vp]),
     "ocx_dev_simulate_smart": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_double, c_vp,
                                        c_vp, c_vp]),
+    "ocx_dev_simulate_smart_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_vp, c_double,
+                                          c_vp, c_vp, c_int, c_vp, c_vp]),
     "ocx_dev_replay": (c_int, [ctypes.POINTER(Layout), ctypes.POINTER(Layout), c_vp, c_vp, c_vp,
                                c_vp, c_vp, c_vp]),
     "ocx_dev_max_regret": (c_int, [c_vp, c_i64, c_vp, c_vp]),
@@ -107,6 +109,7 @@ OCX_VERSION = 200  # include/ocx.h OCX_VERSION: the ABI these signatures describ
 OCX_ALG_CLIPPED_ROWS = 1
 OCX_ALG_CLOSED_COMPARATOR = 2
 OCX_ALG_TREE_SUMS = 4
+OCX_SMART_CLOSED_PREFIX = 8
 
 _lib = None
 _lock = threading.Lock()

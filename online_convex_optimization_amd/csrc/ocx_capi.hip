@@ -403,6 +403,27 @@ int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const dou
     return OCX_OK;
 }
 
+int ocx_dev_simulate_smart_ex(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                              const double* thresh, double eta0, double* regret,
+                              int64_t* switch_step, int flags, unsigned long long* stats,
+                              void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->B && (!thresh || !regret)) return fail(OCX_E_INVALID, "NULL thresh/regret");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
+    if (flags & ~(OCX_SMART_CLOSED_PREFIX | OCX_ALG_CLOSED_COMPARATOR | OCX_ALG_CLIPPED_ROWS))
+        return fail(OCX_E_INVALID, "unknown flags");
+    const int prefix = (flags & OCX_SMART_CLOSED_PREFIX) ? 1 : 0;
+    const int comp = (flags & (OCX_ALG_CLOSED_COMPARATOR | OCX_ALG_CLIPPED_ROWS)) ? 1 : 0;
+    if (!prefix && !comp && !stats) {
+        OCX_HIP(ocx_launch_smart(L, z_tiled, y_tiled, thresh, eta0, regret, switch_step,
+                                 (hipStream_t)stream));
+    } else {
+        OCX_HIP(ocx_launch_smart_closed(L, z_tiled, y_tiled, thresh, eta0, regret, switch_step,
+                                        prefix, comp, stats, (hipStream_t)stream));
+    }
+    return OCX_OK;
+}
+
 int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_tiled,
                    const double* y_tiled, const double* a_tiled, double* cum_loss,
                    double* comp_loss, void* stream) {
@@ -494,8 +515,17 @@ int ocx_simulate_smart_batch(const double* z, const double* y, int64_t B, int64_
     OCX_HIP(hipMemcpyAsync(cx->thr.p, thresh, (size_t)B * 8, hipMemcpyHostToDevice, st));
     OCX_HIP(ocx_launch_pack(&L, cx->zraw.as<double>(), cx->yraw.as<double>(), cx->zt.as<double>(),
                             cx->yt.as<double>(), st));
-    OCX_HIP(ocx_launch_smart(&L, cx->zt.as<double>(), cx->yt.as<double>(), cx->thr.as<double>(),
-                             eta0, cx->out.as<double>(), cx->sw.as<int64_t>(), st));
+    if (lanes_per_seq == 1 || lanes_per_seq < 0) {
+        // bit-exact modes: the reference's prefix re-scan and streamed comparator
+        OCX_HIP(ocx_launch_smart(&L, cx->zt.as<double>(), cx->yt.as<double>(),
+                                 cx->thr.as<double>(), eta0, cx->out.as<double>(),
+                                 cx->sw.as<int64_t>(), st));
+    } else {
+        // O(T·d): guarded closed-form prefix, certified closed-form comparator
+        OCX_HIP(ocx_launch_smart_closed(&L, cx->zt.as<double>(), cx->yt.as<double>(),
+                                        cx->thr.as<double>(), eta0, cx->out.as<double>(),
+                                        cx->sw.as<int64_t>(), 1, 1, nullptr, st));
+    }
     OCX_HIP(hipMemcpyAsync(regret, cx->out.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));
     if (switch_step)
         OCX_HIP(hipMemcpyAsync(switch_step, cx->sw.p, (size_t)B * 8, hipMemcpyDeviceToHost, st));

@@ -16,6 +16,14 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);
+// SMART in O(T·d) (ocx_smart_closed.hip): closed_prefix decides the switch from the
+// closed-form prefix loss outside a rounding guard band (re-scan inside it: the reference's
+// decisions); closed_comp takes the final comparator loss in closed form where certified.
+// stats (nullable, device [2]): += re-scanned steps, += sequences with the closed comparator
+hipError_t ocx_launch_smart_closed(const ocx_layout* L, const double* zt, const double* yt,
+                                   const double* th, double eta0, double* reg, int64_t* sw,
+                                   int closed_prefix, int closed_comp, unsigned long long* stats,
+                                   hipStream_t st);
 // SMART with one wavefront per sequence (ocx_smart_wave.hip), d <= 64
 hipError_t ocx_launch_smart_wave(const ocx_layout* L, const double* zt, const double* yt,
                                  const double* th, double eta0, double* reg, int64_t* sw,

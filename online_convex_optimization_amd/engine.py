@@ -78,7 +78,10 @@ def simulate_alg_batch(z, y, alg_flag: int = 0, eta0: float = SQRT2, comparator=
 
 def simulate_smart_batch(z, y, thresh, eta0: float = SQRT2, *, lanes_per_seq: int = LANES_BEST,
                          device: int = 0, return_switch: bool = False):
-    """fast_algorithms.py:118-164 over B sequences; thresh scalar or [B]."""
+    """fast_algorithms.py:118-164 over B sequences; thresh scalar or [B].  Bit-exact modes
+    (lanes_per_seq 1 / -k) run the reference's O(T²·d) prefix re-scan; the others the
+    O(T·d) kernel (guarded closed-form prefix: the same switch steps; closed-form final
+    comparator where certified: the regret within its rounding)."""
     z = _f64(z)
     y = _f64(y)
     B, T, d = _check_zy(z, y)
@@ -461,13 +464,31 @@ class DeviceBatch:
                   closed_out.data_ptr() if closed_out is not None else None, self._sp)
         return self.regret
 
-    def simulate_smart(self, thresh, eta0: float = SQRT2, switch_step=None):
+    def simulate_smart(self, thresh, eta0: float = SQRT2, switch_step=None,
+                       closed_prefix: Optional[bool] = None,
+                       closed_comparator: Optional[bool] = None, stats=None):
+        """SMART (fast_algorithms.py:118-164) on the resident batch; thresh scalar or [B].
+
+        ``closed_prefix`` (default: not a bit-exact layout) runs in O(T·d): the pre-switch
+        prefix loss in closed form, deciding the switch only outside a rounding guard band
+        and re-scanning the prefix inside it (the reference's switch steps; see
+        include/ocx.h, OCX_SMART_CLOSED_PREFIX).  ``closed_comparator`` (same default) takes
+        the final comparator loss in closed form where certified.  ``stats`` ([2] uint64
+        (int64) device tensor, optional) accumulates re-scanned steps and closed-comparator
+        sequences."""
         with self._on_stream():
             th = self.torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
                                                       (self.L.B,)).copy()).to(self.device)
         sp = switch_step.data_ptr() if switch_step is not None else None
-        _lib.call("ocx_dev_simulate_smart", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
-                  th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, self._sp)
+        if closed_prefix is None:
+            closed_prefix = not self.exact
+        if closed_comparator is None:
+            closed_comparator = not self.exact
+        flags = ((_lib.OCX_SMART_CLOSED_PREFIX if closed_prefix else 0) |
+                 (_lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0))
+        _lib.call("ocx_dev_simulate_smart_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+                  th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, flags,
+                  stats.data_ptr() if stats is not None else None, self._sp)
         self._keep_th = self._hold(th)
         return self.regret
 
