@@ -22,7 +22,7 @@ BUILD = os.path.join(ROOT, "build", "ocx")
 LIB = os.path.join(PKG, "libocx.so")
 ARCH = os.environ.get("OCX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["ocx_sim.hip", "ocx_smart_wave.hip", "ocx_smart_closed.hip", "ocx_ftrl_exact.hip", "ocx_gen.hip",
+SOURCES = ["ocx_sim.hip", "ocx_alg_pipe.hip", "ocx_smart_wave.hip", "ocx_smart_closed.hip", "ocx_ftrl_exact.hip", "ocx_gen.hip",
            "ocx_gen_wave.hip", "ocx_stream.hip", "ocx_twin32.hip", "ocx_comp_blas.hip", "ocx_capi.hip"]
 HEADERS = ["../../include/ocx_testing.h", "ocx_internal.h", "ocx_rng.h", "ocx_sim_kernels.h", "zig_tables.h",
            "ocx_device_math.h", "ocx_dispatch.h"]
@@ -74,12 +74,13 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
     return LIB
 
 
-def build_variant(name: str, defines, jobs: int = 4, source: str = "ocx_sim.hip") -> str:
+def build_variant(name: str, defines, jobs: int = 4, source: str = "ocx_sim.hip",
+                  out_dir: str = None) -> str:
     """Tuning variant: one source recompiled with -D overrides, linked with the other
-    objects into tune_build/libocx_<name>.so (never loaded by the product path; select it
-    with OCX_LIB)."""
+    objects into <out_dir, default tune_build>/libocx_<name>.so (never loaded by the product
+    path; select it with OCX_LIB)."""
     hipcc = _hipcc()
-    out_dir = os.path.join(ROOT, "tune_build")
+    out_dir = out_dir or os.path.join(ROOT, "tune_build")
     os.makedirs(out_dir, exist_ok=True)
     build(jobs=jobs)  # the shared objects of the other sources
     obj = os.path.join(out_dir, f"{source.replace('.hip', '')}_{name}.o")

@@ -1,0 +1,231 @@
+// ocx_alg_pipe.hip — FTRL/FTL (fast_algorithms.py:88-115) for the butterfly-sum layouts
+// (P >= 2 lanes per sequence, chain = 0) with the step's dependency chain cut short.
+//
+// In the plain kernel (ocx_sim.hip) step t waits for g_{t-1}, then forms x = sθ_t, sums
+// ||x||² and z_t·x lane by lane (C dependent adds each), crosses the P lanes, and — when
+// the FTRL action is rescaled, which on the g(T) adversary is most steps — sums z_t·x a
+// second time: about 60 dependent fp64 operations, ≈1 100 cycles per step.  A few-wave
+// batch (capacity-limited long horizons: d = 64, T = 1e5, ≈4 900 sequences, one wave per
+// SIMD) cannot hide that, so its time is T × that latency.
+//
+// Here every lane-local product of step t is formed BEFORE g_{t-1} is known, from the
+// lagging state θ' = θ_{t-1} (θ_t = θ' + g_{t-1} z_{t-1}):
+//     A = z_t·θ',  Bz = z_t·z_{t-1},  U = θ'·θ',  V = θ'·z_{t-1},  W = z_{t-1}·z_{t-1}
+// (per lane, over its C coordinates), so that once g = g_{t-1} arrives
+//     z_t·θ_t = A + g·Bz,   ||θ_t||² = U + g·(2V + g·W)
+// are one or two fma per lane, then the P-lane butterflies; FTRL's action follows as
+//     s_abs = |s_t|·sqrt(||θ_t||²),  f = 1/s_abs if s_abs > 1 else 1,  q = (s_t·(z_t·θ_t))·f
+// and FTL's as q = (−1/sqrt(||θ_t||²))·(z_t·θ_t) (0 when θ_t = 0).  The chain is ≈25
+// dependent operations; the C-wide products run beside it.  θ itself is updated exactly
+// as the reference does (θ += g·z, g a power of two), so the trajectory is the
+// reference's; each step's q carries the butterfly layouts' usual ~1e-16 relative
+// rounding difference (tests/test_gpu_parity.py: 1e-12 bar).  For rows with a single
+// nonzero coordinate (the flip / switching families, exact ties) every quantity above
+// is exact and equal to the reference's (sqrt of an exact square is exact; s_abs =
+// |fl(s θ_j)| and f = fl(1/s_abs) then reproduce the reference's rescale bit for bit).
+// FTL near θ = 0, where ||θ_t||² = U + g(2V + gW) would lose relative accuracy to
+// cancellation, re-sums ||θ_t||² directly (||θ_t||² < 0.25: early steps, returns to the
+// origin).  The comparator pass / closed form are those of ocx_alg_kernel.
+#include "ocx_device_math.h"
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+template <int C, int P, int NB>
+__global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t G, int ftl, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
+    double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass) {
+    static_assert(P >= 2 && NB >= 2, "butterfly layouts, a ring holding z_{t+1}");
+    constexpr int S = 64 / P;
+    constexpr int K = C / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t g = ocx_wave_id();
+    if (g >= G) return;
+    const int s = lane / P;
+    const int c = lane % P;
+    const int64_t b = g * S + s;
+    const int64_t tstride = 64;  // ocx_d2 per step within a plane
+    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const int64_t kst = G * T * 64;  // plane stride (pairs k)
+    const double* __restrict__ yp = yt + g * T * S + s;
+    bool clean = true;  // onepass: rows in the ball, every sub-gradient −y_t/2
+
+    double th[C], zprev[C];  // θ_{t-1} (lagging one update) and z_{t-1}
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = zprev[j] = 0.0;
+    double gp = 0.0;                                   // g_{t-1}
+    double A = 0.0, Bz = 0.0, U = 0.0, V = 0.0, W = 0.0;  // step t's lane partials
+
+    ocx_d2 zb[NB][K];
+    double yb[NB];
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u)
+        if (u < T) {
+            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+            yb[u] = yp[u * S];
+        }
+    // step 0's A and Bz: θ' = 0, z_{-1} = 0
+    double cum = 0.0;
+    OcxScaleTable sct;
+    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int64_t t = t0 + u;
+            if (t < T) {
+                // ---- chain: g_{t-1} → z_t·θ_t, ||θ_t||² → q_t → g_t
+                const double zth = __builtin_fma(gp, Bz, A);
+                const double tth = __builtin_fma(gp, __builtin_fma(gp, W, 2.0 * V), U);
+                // θ_t = θ_{t-1} + g_{t-1} z_{t-1} (exact: g is a power of two or 0)
+#pragma unroll
+                for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
+                const int64_t tp = t + NB - 1;
+                if (tp < T) {
+                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                    yb[(u + NB - 1) % NB] = yp[tp * S];
+                }
+                const double q_raw = ocx_seq_sum<P>(zth);
+                double n_raw = ocx_seq_sum<P>(tth);
+                double q;
+                if (!ftl) {
+                    const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);  // −η0/√t
+                    const double a = sc * q_raw;
+                    const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+                    q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
+                } else {
+                    if (n_raw < 0.25) {  // near θ = 0: re-sum directly (see above)
+                        double p[C];
+#pragma unroll
+                        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+                        n_raw = ocx_seq_sum<P>(ocx_lane_sum<C>(p));
+                    }
+                    q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
+                }
+                const double yv = yb[u];
+                const double diff = q - yv;  // :106-111
+                cum += 0.5 * fabs(diff);
+                const double gq = ocx_grad(diff);
+                clean = clean && fabs(yv) == 1.0 && gq == -0.5 * yv;
+
+                // ---- off the chain: step t+1's lane partials (θ_t is known, g_t is not)
+                const ocx_d2* zc = zb[u];
+                const ocx_d2* zn = zb[(u + 1) % NB];  // z_{t+1}, loaded NB-1 steps ago
+                double w = 0.0, uu = 0.0, an = 0.0, bn = 0.0;
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const double zj = ocx_zj(zc, j);
+                    w = __builtin_fma(zj, zj, w);
+                    uu = __builtin_fma(th[j], th[j], uu);
+                    an = __builtin_fma(ocx_zj(zn, j), th[j], an);
+                    bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
+                    zprev[j] = zj;
+                }
+                if (onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
+                V = zth;
+                W = w;
+                U = uu;
+                A = t + 1 < T ? an : 0.0;
+                Bz = t + 1 < T ? bn : 0.0;
+                gp = gq;
+            }
+        }
+    }
+    // θ_T = θ_{T-1} + g_{T-1} z_{T-1}
+#pragma unroll
+    for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
+
+    // ---- comparator: closed form where certified (ocx_alg_kernel onepass), else the
+    // reference's second streaming pass with x* = FTL(θ_T) (fast_algorithms.py:113-114)
+    const bool closed = onepass && (clean || b >= B);
+    double comp = 0.0;
+    if (__ballot(!closed) != 0) {  // wave-uniform
+        double xs[C];
+        ocx_action_ftl<C, P, false>(th, xs, lane);
+#pragma unroll
+        for (int u = 0; u < NB - 1; ++u)
+            if (u < T) {
+                ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
+                yb[u] = yp[u * S];
+            }
+        for (int64_t t0 = 0; t0 < T; t0 += NB) {
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int64_t t = t0 + u;
+                if (t < T) {
+                    const int64_t tp = t + NB - 1;
+                    if (tp < T) {
+                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
+                        yb[(u + NB - 1) % NB] = yp[tp * S];
+                    }
+                    double p[C];
+#pragma unroll
+                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
+                    const double qq = ocx_total<C, P, false>(p, lane);
+                    comp += 0.5 * fabs(qq - yb[u]);
+                }
+            }
+        }
+    }
+    if (__ballot(closed) != 0) {
+        double p[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+        const double nrm = sqrt(ocx_total<C, P, false>(p, lane));
+        if (closed) comp = 0.5 * (double)T - nrm;
+    }
+    if (c == 0 && b < B) {
+        if (regret) regret[b] = cum - comp;
+        if (cum_out) cum_out[b] = cum;
+        if (comp_out) comp_out[b] = comp;
+        if (closed_out) closed_out[b] = closed ? 1 : 0;
+    }
+}
+
+namespace {
+template <int C, int P>
+hipError_t launch_pipe_cp(const ocx_layout* L, const double* zt, const double* yt, int ftl,
+                          double eta0, double* reg, double* cum, double* comp, int* closed_out,
+                          int onepass, hipStream_t st) {
+    // z_{t+1} must be in the ring a step ahead: at least three steps in flight
+    constexpr int NB = nb_for(C, P) < 3 ? 3 : nb_for(C, P);
+    hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB>), ocx_grid(L->G, ocx_block_waves(L->G)),
+                       dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->G, ftl, eta0,
+                       reg, cum, comp, closed_out, onepass);
+    return hipGetLastError();
+}
+
+template <int C>
+hipError_t launch_pipe_c(const ocx_layout* L, const double* zt, const double* yt, int ftl,
+                         double eta0, double* reg, double* cum, double* comp, int* closed_out,
+                         int onepass, hipStream_t st) {
+    switch (L->P) {
+        case 2: return launch_pipe_cp<C, 2>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 4: return launch_pipe_cp<C, 4>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 8: return launch_pipe_cp<C, 8>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 16: return launch_pipe_cp<C, 16>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 32: return launch_pipe_cp<C, 32>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 64: return launch_pipe_cp<C, 64>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+bool ocx_pipe_supported(const ocx_layout* L) {
+    return !L->chain && L->P >= 2 && L->C <= 32;
+}
+
+hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const double* yt, int ftl,
+                               double eta0, double* reg, double* cum, double* comp,
+                               int* closed_out, int onepass, hipStream_t st) {
+    if (L->G == 0) return hipSuccess;
+    switch (L->C) {
+        case 2: return launch_pipe_c<2>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 4: return launch_pipe_c<4>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 6: return launch_pipe_c<6>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 8: return launch_pipe_c<8>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 12: return launch_pipe_c<12>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 16: return launch_pipe_c<16>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 24: return launch_pipe_c<24>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        case 32: return launch_pipe_c<32>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
+        default: return hipErrorInvalidValue;
+    }
+}

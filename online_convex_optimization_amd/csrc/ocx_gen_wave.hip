@@ -32,6 +32,11 @@ namespace {
 
 constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 
+// Float fast path of the ziggurat's wedge test (see zig_round); 0 = the double form.
+#ifndef OCX_GEN_WEDGE_F32
+#define OCX_GEN_WEDGE_F32 1
+#endif
+
 struct ZigTables {
     uint64_t ki[256];
     double wi[256];
@@ -120,10 +125,14 @@ __device__ __noinline__ TailOut zig_tail(uint64_t st_lo, uint64_t st_hi, uint64_
 }
 
 // One stream, as a wave sees it: the uniform state and increment, and this lane's
-// jump-ahead pair (state after draw k of a round = Ak * base + Dk).
+// jump-ahead pair (state after draw k of a round = Ak * base + Dk).  spec: this lane's
+// state of the NEXT round, formed ahead from lane 63's state (valid when `have_spec`, i.e.
+// the round consumed all 64 draws, which 99 % of rounds do).
 struct WaveStream {
     ocx_u128 base, inc;
     ocx_u128 Ak, Dk;
+    ocx_u128 spec;
+    bool have_spec;
 };
 
 // ---- (a * b + d) mod 2^128 with a, d per lane and b wave-uniform (SGPRs) --------------
@@ -159,7 +168,9 @@ __device__ __forceinline__ uint32_t addc32z(uint32_t a, uint64_t cin) {
     return r;
 }
 __device__ __forceinline__ ocx_u128 mul_add_u128(ocx_u128 a, ocx_u128 b, ocx_u128 d) {
-#ifdef OCX_GEN_INT128_MUL  // reference form (tuning A/B)
+#if defined(OCX_GEN_TUNE_CHEAP_MUL)  // tuning only: no multiply (wrong normals)
+    return (a ^ b) + d;
+#elif defined(OCX_GEN_INT128_MUL)  // reference form (tuning A/B)
     return a * b + d;
 #else
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), a2 = (uint32_t)(a >> 64),
@@ -191,6 +202,7 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
     w.base = rl128(g.state, 0);
     w.inc = g.inc;
     w.Dk = g.inc * Gk;
+    w.have_spec = false;
 }
 
 // One round: speculate 64 draws, parse them in stream order, append at most `need`
@@ -198,10 +210,28 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 // the stream past exactly the draws those normals consumed (NumPy random_standard_normal).
 // FULL: need == 64 is known (every round of a d = 64 row stream but the last): a rejection
 // round then appends at most 63 normals, so the need-capping tail below drops out.
+// Speculative next-round state (OCX_GEN_SPEC_NEXT, default on): the next round's
+// multiply-add is issued right after this round's, from lane 63's state, so it overlaps
+// this round's table lookup, test and parse instead of waiting behind them; a round that
+// stops short of draw 63 (a rejected lane 63, a tail draw, the last round) drops it.
+#ifndef OCX_GEN_SPEC_NEXT
+#define OCX_GEN_SPEC_NEXT 1
+#endif
 template <bool RING, bool FULL = false>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
+#if OCX_GEN_SPEC_NEXT
+    ocx_u128 s;
+    if (w.have_spec) {  // wave-uniform
+        s = w.spec;
+    } else {
+        s = mul_add_u128(w.Ak, w.base, w.Dk);
+    }
+    const ocx_u128 s63 = rl128(s, 63);
+    w.spec = mul_add_u128(w.Ak, s63, w.Dk);
+#else
     const ocx_u128 s = mul_add_u128(w.Ak, w.base, w.Dk);
+#endif
     const uint64_t r = xsl_rr(s);
     const int idx = (int)(r & 0xff);
     const uint64_t r8 = r >> 8;
@@ -218,7 +248,12 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const uint64_t rej = ballot(!fast);
     if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
         if (RING) ring[(head + (unsigned)lane) & rmask] = x;
+#if OCX_GEN_SPEC_NEXT
+        w.base = s63;
+        w.have_spec = true;
+#else
         w.base = rl128(s, 63);
+#endif
         return 64;
     }
     uint64_t cons = 0, wacc = 0;
@@ -232,6 +267,29 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #else
         if (!fast && idx != 0) {
 #endif
+#if OCX_GEN_WEDGE_F32
+        }
+        {
+            // Every lane evaluates a float estimate of both sides (no exec-mask branch; the
+            // rejected lanes' results are kept): lhs = (fi[idx-1] − fi[idx])·u + fi[idx]
+            // with u from the top 32 bits of the next draw, and exp(−x²/2) by v_exp_f32,
+            // each within 3e-6 relative, decided with a 1e-5 margin; a lane too close to
+            // call (~1e-5 of wedge tests) takes NumPy's double arithmetic below.
+            const int i1 = idx ? idx : 1;
+            const float f1 = (float)tb.fi[i1 - 1], f0 = (float)tb.fi[i1];
+            const float u = (float)(uint32_t)(rn >> 32) * 2.3283064365386963e-10f;  // 2^-32
+            const float lhs_f = fmaf(f1 - f0, u, f0);
+            const float xf = (float)x;
+            const float e = __expf(-0.5f * xf * xf);
+            const bool cand = !fast && idx != 0;
+            wa = cand && lhs_f < e * (1.0f - 1e-5f);
+            const bool unsure = cand && !wa && !(lhs_f > e * (1.0f + 1e-5f));
+            if (ballot(unsure) != 0 && unsure) {
+                const double lhs = (tb.fi[idx - 1] - tb.fi[idx]) * u53(rn) + tb.fi[idx];
+                wa = wedge_exact(lhs, -0.5 * x * x);
+            }
+        }
+#else
             const double lhs = (tb.fi[idx - 1] - tb.fi[idx]) * u53(rn) + tb.fi[idx];
             const double a = -0.5 * x * x;
             const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
@@ -239,6 +297,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
             else if (lhs > e * (1.0 + 1e-5)) wa = false;
             else wa = wedge_exact(lhs, a);
         }
+#endif
         wacc = ballot(wa);
         const uint64_t tailm = ballot(!fast && idx == 0);
         // Usual case: no tail draw and no two rejected draws side by side, so every
@@ -291,9 +350,22 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
                                    (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
         if (RING && lane == 0) ring[(head + n) & rmask] = o.v;
         w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
+#if OCX_GEN_SPEC_NEXT
+        w.have_spec = false;
+#endif
         return n + 1;
     }
+#if OCX_GEN_SPEC_NEXT
+    if (m == 64) {  // the next round starts from lane 63's state: the speculation holds
+        w.base = s63;
+        w.have_spec = true;
+    } else {
+        w.base = rl128(s, m - 1);
+        w.have_spec = false;
+    }
+#else
     w.base = rl128(s, m - 1);
+#endif
     return n;
 }
 

@@ -530,6 +530,15 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
                           double* xl, hipStream_t st, double* cmp_out, int* regime, int onepass,
                           int norm) {
     if (L->G == 0) return hipSuccess;
+    // butterfly layouts: the pipelined step (ocx_alg_pipe.hip) unless an input comparator,
+    // x_last or the comparator action is asked for (OCX_ALG_NO_PIPE=1: the plain kernel,
+    // for A/B measurements)
+    static const bool no_pipe = [] {
+        const char* e = std::getenv("OCX_ALG_NO_PIPE");
+        return e && std::atoi(e) != 0;
+    }();
+    if ((algo == 0 || algo == 1) && !cmp && !xl && !cmp_out && !no_pipe && ocx_pipe_supported(L))
+        return ocx_launch_alg_pipe(L, zt, yt, algo, eta0, reg, cum, comp, regime, onepass, st);
     OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
                  onepass, norm, st)
 }

@@ -13,6 +13,12 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
                           double eta0, const double* cmp, double* reg, double* cum, double* comp,
                           double* xl, hipStream_t st, double* cmp_out = nullptr,
                           int* regime = nullptr, int onepass = 0, int norm = 0);
+// FTRL / FTL for butterfly layouts (chain = 0, P >= 2, C <= 32) with the step's dependency
+// chain cut short (ocx_alg_pipe.hip); no comparator input, x_last or comparator output
+bool ocx_pipe_supported(const ocx_layout* L);
+hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const double* yt, int ftl,
+                               double eta0, double* reg, double* cum, double* comp,
+                               int* closed_out, int onepass, hipStream_t st);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

@@ -377,12 +377,17 @@ def test_driver_stats_golden(ocx, golden):
                                          (130, 100, 20, 0), (37, 1024, 6, 0), (211, 64, 33, 1)])
 def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
     """A tiny HBM budget forces the T-chunked path (seek → pass A → pass B with saved PCG
-    states): regrets must equal the single-launch path bit for bit."""
+    states): regrets must equal the single-launch path bit for bit in the exact modes; in
+    the butterfly mode (P = 0) the single launch runs the pipelined step (ocx_alg_pipe.hip)
+    and the chunks the plain one, so they agree to the butterfly bar."""
     eng = ocx["engine"]
     whole = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
     monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(200e3 / 2**30))  # ~200 KB → many chunks
     chunked = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
-    assert np.array_equal(whole, chunked)
+    if P == 0:
+        assert close(chunked, whole)
+    else:
+        assert np.array_equal(whole, chunked)
     for r in (0, runs - 1):
         z, y = O.gT_sample(4, T, 7 + r, d)
         ref = O.simulate_alg(z, y, 0, SQ2)
@@ -700,13 +705,20 @@ def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
     monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(200e3 / 2**30))  # ~200 KB → streamed
     monkeypatch.setenv("OCX_MIN_RESIDENT", str(1 << 30))
     plain = eng.gT_regrets(T, runs, base_seed=4, d=d, run0=7, lanes_per_seq=P)
-    assert np.array_equal(plain, closed)
+    # butterfly layouts (both cases here): the resident launch is the pipelined kernel, the
+    # chunks the plain one (test_streamed_gT_matches_resident): equal to the 1e-12 bar
+    def same(a, b):
+        return close(a, b)
+    assert same(plain, closed)
     lib = ocx["lib"]
     mixed = np.zeros(runs)
     lib.call("ocx_test_gT_regrets_unclean", 4, T, 7, runs, d, SQ2, lib.ptr(mixed), P, 0, 3)
     marked = np.arange(runs) % 3 == 0
-    assert np.array_equal(mixed[marked], two[marked])
-    assert np.array_equal(mixed[~marked], closed[~marked])
+    assert same(mixed[marked], two[marked])
+    assert same(mixed[~marked], closed[~marked])
+    # the marked runs really took the streamed second pass: bit-equal to a two-pass run of
+    # the same (chunked) kernel family, i.e. not the closed form
+    assert not np.array_equal(mixed[marked], closed[marked])
 
 
 @pytest.mark.parametrize("T,d", [(1, 3), (1, 20), (2, 8), (3, 5), (7, 13), (130, 5), (9000, 5),

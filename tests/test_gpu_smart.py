@@ -82,7 +82,8 @@ def test_closed_prefix_matches_rescan_on_sampler_rows(eng):
     import torch
     B, T, d = 512, 1500, 8
     rng = np.random.default_rng(12)
-    th = rng.uniform(-1.0, 8.0, size=B)
+    th = rng.uniform(-1.0, 30.0, size=B)
+    th[::7] = 1e9  # never switches: the whole horizon stays pre-switch
     db = eng.DeviceBatch(B, T, d, lanes_per_seq=1).generate_gT(base_seed=11)
     out = {}
     for key, (pf, cc) in {"rescan": (False, False), "prefix": (True, False),

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=1)
     ap.add_argument("--variants", default="")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--dir", default="tune_build", help="where the variant libraries are")
     a = ap.parse_args()
     import torch
     from online_convex_optimization_amd import _lib, engine
@@ -30,7 +31,7 @@ def main():
     db = engine.DeviceBatch(a.B, a.T, a.d, lanes_per_seq=a.lanes)
     libs = [("base", _lib.load())]
     for v in [x for x in a.variants.split(",") if x]:
-        L = ctypes.CDLL(os.path.join(ROOT, "tune_build", f"libocx_{v}.so"))
+        L = ctypes.CDLL(os.path.join(ROOT, a.dir, f"libocx_{v}.so"))
         L.ocx_dev_gen_gT.argtypes = _lib.SIGNATURES["ocx_dev_gen_gT"][1]
         libs.append((v, L))
     res = {n: [] for n, _ in libs}
