@@ -45,10 +45,12 @@
 #define OCX_H_
 
 #define OCX_LANES_BEST 128
-/* ocx_version() == OCX_VERSION = 10000 * major + 100 * minor + patch (200 = 0.2.0).  0.2.0:
+/* ocx_version() == OCX_VERSION = 10000 * major + 100 * minor + patch (300 = 0.3.0).  0.2.0:
  * ocx_ftrl_vs_exact_batch has its round-1 signature again (the `norm` argument moved to
- * ocx_ftrl_vs_exact_batch_ex); callers built against 0.1.x check ocx_version() >= 200. */
-#define OCX_VERSION 200
+ * ocx_ftrl_vs_exact_batch_ex); callers built against 0.1.x check ocx_version() >= 200.
+ * 0.3.0 adds the general exact-FTL solver (ocx_exact_ball_solve, ocx_dev_exact_ball_solve,
+ * ocx_dev_exact_ball_solve_tiled); nothing existing changed. */
+#define OCX_VERSION 300
 
 #include <stddef.h>
 #include <stdint.h>
@@ -165,6 +167,27 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
                                double eta0, double* cum_ftrl, double* cum_exact,
                                double* comp_exact, double* comp_ftl, double* cmp_action,
                                int32_t* regime, int norm, int lanes_per_seq, int device);
+
+/* The general exact-FTL comparator: ExactFTLNoClip's problem (exact_ftl.py:83-105,
+ * solved with cvxpy at :119-128)
+ *     min_x ½ Σ_{i<n} |z_i·x − y_i|   s.t.  ||x||_norm <= 1   (norm 0 l2, 1 l1, 2 linf)
+ * for any rows and labels (no regime: where the closed forms above do not apply), on device
+ * by a primal log-barrier path (damped Newton, μ from 1 to 1e-10).  Where
+ * the minimiser is not unique the path's limit, the analytic centre of the optimal face, is
+ * returned.  Problems: each sequence's prefixes n = 0..T (all_prefixes = 1, actions
+ * [B][T+1][d] as compute_prefix_actions :280-303 returns; actions[b][0] = 0) or n = T only
+ * (all_prefixes = 0, [B][1][d]: the comparator).  obj [B][NP] (nullable) = ½Σ|r| at x
+ * (for n = T: the comparator loss, exact_ftl.py:224-227, in butterfly order); gap [B][NP]
+ * (nullable) = obj minus a dual lower bound (a certificate: obj − optimum <= gap);
+ * step_loss [B][NP] (nullable) = ½|z_n·x_n − y_n|, what FTL pays at step n with the prefix-n
+ * action (replay_exact_ftl :318-323; 0 for n = T), so Σ_n step_loss is exact FTL's cumulative
+ * loss; info [B][NP] (int32, nullable) = Newton steps, negated if the 300-step cap ended the
+ * solve.  1 <= d <= OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy:
+ * unpinned (validated against scipy's HiGHS LPs and by the certificate). */
+#define OCX_EXACT_BALL_MAX_D 10
+int ocx_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                         int norm, int all_prefixes, double* actions, double* obj, double* gap,
+                         double* step_loss, int32_t* info, int device);
 
 /* exact_ftl.py:306-333 replay_exact_ftl, batched: actions [B][T+1][d].
  * cum_loss = sum_{t<T} 0.5|z_t.a_t - y_t|; comp_loss = sum_t 0.5|z_t.a_T - y_t|. */
@@ -350,6 +373,17 @@ int ocx_dev_simulate_smart_ex(const ocx_layout* L, const double* z_tiled, const 
 int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_tiled,
                    const double* y_tiled, const double* a_tiled, double* cum_loss,
                    double* comp_loss, void* stream);
+
+/* ocx_exact_ball_solve on device: z [B][T][d], y [B][T] row-major (device), outputs as
+ * there (device); runs on `stream`, does not synchronise. */
+int ocx_dev_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                             int norm, int all_prefixes, double* actions, double* obj, double* gap,
+                             double* step_loss, int32_t* info, void* stream);
+/* The same on a resident batch in the tiled layout L. */
+int ocx_dev_exact_ball_solve_tiled(const ocx_layout* L, const double* z_tiled,
+                                   const double* y_tiled, int norm, int all_prefixes,
+                                   double* actions, double* obj, double* gap, double* step_loss,
+                                   int32_t* info, void* stream);
 
 /* Max over runs of regrets[B] (device) into *gmax (device), starting from 0.0
  * as fast_algorithms.py:228,242-243 does. */

@@ -98,6 +98,12 @@ SIGNATURES = {
     "ocx_dev_twin32": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp, c_vp,
                                c_vp, c_vp, c_vp, c_vp]),
     "ocx_twin32_gT_regrets": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_fp, c_int]),
+    "ocx_exact_ball_solve": (c_int, [c_dp, c_dp, c_i64, c_i64, c_i64, c_int, c_int, c_dp, c_dp,
+                                     c_dp, c_dp, ctypes.POINTER(ctypes.c_int32), c_int]),
+    "ocx_dev_exact_ball_solve": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, c_int, c_int, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp]),
+    "ocx_dev_exact_ball_solve_tiled": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_int,
+                                               c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 }
 # include/ocx_testing.h: test-only entry points (bound like the others, never called by the
 # package itself)
@@ -105,8 +111,9 @@ TEST_SIGNATURES = {
     "ocx_test_gT_regrets_unclean": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp,
                                             c_int, c_int, c_i64]),
 }
-OCX_VERSION = 200  # include/ocx.h OCX_VERSION: the ABI these signatures describe
+OCX_VERSION = 300  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1
+OCX_EXACT_BALL_MAX_D = 10  # include/ocx.h
 OCX_ALG_CLOSED_COMPARATOR = 2
 OCX_ALG_TREE_SUMS = 4
 OCX_SMART_CLOSED_PREFIX = 8

@@ -58,77 +58,63 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
 
     ocx_d2 zb[NB][K];
     double yb[NB];
-#pragma unroll
-    for (int u = 0; u < NB - 1; ++u)
-        if (u < T) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
-            yb[u] = yp[u * S];
-        }
-    // step 0's A and Bz: θ' = 0, z_{-1} = 0
+    auto load = [&](int slot, int64_t tl) {
+        ocx_load_tile<C>(zb[slot], zp + tl * tstride, kst);
+        yb[slot] = yp[tl * S];
+    };
     double cum = 0.0;
     OcxScaleTable sct;
-    for (int64_t t0 = 0; t0 < T; t0 += NB) {
+    ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+        // ---- chain: g_{t-1} → z_t·θ_t, ||θ_t||² → q_t → g_t
+        const double zth = __builtin_fma(gp, Bz, A);
+        const double tth = __builtin_fma(gp, __builtin_fma(gp, W, 2.0 * V), U);
+        // θ_t = θ_{t-1} + g_{t-1} z_{t-1} (exact: g is a power of two or 0)
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int64_t t = t0 + u;
-            if (t < T) {
-                // ---- chain: g_{t-1} → z_t·θ_t, ||θ_t||² → q_t → g_t
-                const double zth = __builtin_fma(gp, Bz, A);
-                const double tth = __builtin_fma(gp, __builtin_fma(gp, W, 2.0 * V), U);
-                // θ_t = θ_{t-1} + g_{t-1} z_{t-1} (exact: g is a power of two or 0)
+        for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
+        const double q_raw = ocx_seq_sum<P>(zth);
+        double n_raw = ocx_seq_sum<P>(tth);
+        double q;
+        if (!ftl) {
+            const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);  // −η0/√t
+            const double a = sc * q_raw;
+            const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+            q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
+        } else {
+            if (n_raw < 0.25) {  // near θ = 0: re-sum directly (see above)
+                double p[C];
 #pragma unroll
-                for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
-                const int64_t tp = t + NB - 1;
-                if (tp < T) {
-                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                    yb[(u + NB - 1) % NB] = yp[tp * S];
-                }
-                const double q_raw = ocx_seq_sum<P>(zth);
-                double n_raw = ocx_seq_sum<P>(tth);
-                double q;
-                if (!ftl) {
-                    const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);  // −η0/√t
-                    const double a = sc * q_raw;
-                    const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
-                    q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
-                } else {
-                    if (n_raw < 0.25) {  // near θ = 0: re-sum directly (see above)
-                        double p[C];
-#pragma unroll
-                        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
-                        n_raw = ocx_seq_sum<P>(ocx_lane_sum<C>(p));
-                    }
-                    q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
-                }
-                const double yv = yb[u];
-                const double diff = q - yv;  // :106-111
-                cum += 0.5 * fabs(diff);
-                const double gq = ocx_grad(diff);
-                clean = clean && fabs(yv) == 1.0 && gq == -0.5 * yv;
-
-                // ---- off the chain: step t+1's lane partials (θ_t is known, g_t is not)
-                const ocx_d2* zc = zb[u];
-                const ocx_d2* zn = zb[(u + 1) % NB];  // z_{t+1}, loaded NB-1 steps ago
-                double w = 0.0, uu = 0.0, an = 0.0, bn = 0.0;
-#pragma unroll
-                for (int j = 0; j < C; ++j) {
-                    const double zj = ocx_zj(zc, j);
-                    w = __builtin_fma(zj, zj, w);
-                    uu = __builtin_fma(th[j], th[j], uu);
-                    an = __builtin_fma(ocx_zj(zn, j), th[j], an);
-                    bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
-                    zprev[j] = zj;
-                }
-                if (onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
-                V = zth;
-                W = w;
-                U = uu;
-                A = t + 1 < T ? an : 0.0;
-                Bz = t + 1 < T ? bn : 0.0;
-                gp = gq;
+                for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+                n_raw = ocx_seq_sum<P>(ocx_lane_sum<C>(p));
             }
+            q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
         }
-    }
+        const double yv = yb[u];
+        const double diff = q - yv;  // :106-111
+        cum += 0.5 * fabs(diff);
+        const double gq = ocx_grad(diff);
+        clean = clean && fabs(yv) == 1.0 && gq == -0.5 * yv;
+
+        // ---- off the chain: step t+1's lane partials (θ_t is known, g_t is not)
+        const ocx_d2* zc = zb[u];
+        const ocx_d2* zn = zb[(u + 1) % NB];  // z_{t+1}, in flight since NB-2 steps
+        double w = 0.0, uu = 0.0, an = 0.0, bn = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            const double zj = ocx_zj(zc, j);
+            w = __builtin_fma(zj, zj, w);
+            uu = __builtin_fma(th[j], th[j], uu);
+            an = __builtin_fma(ocx_zj(zn, j), th[j], an);
+            bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
+            zprev[j] = zj;
+        }
+        if (onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
+        V = zth;
+        W = w;
+        U = uu;
+        A = t + 1 < T ? an : 0.0;
+        Bz = t + 1 < T ? bn : 0.0;
+        gp = gq;
+    });
     // θ_T = θ_{T-1} + g_{T-1} z_{T-1}
 #pragma unroll
     for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
@@ -140,30 +126,13 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
     if (__ballot(!closed) != 0) {  // wave-uniform
         double xs[C];
         ocx_action_ftl<C, P, false>(th, xs, lane);
+        ocx_ring_loop<NB>(T, load, [&](int u, int64_t) {
+            double p[C];
 #pragma unroll
-        for (int u = 0; u < NB - 1; ++u)
-            if (u < T) {
-                ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
-                yb[u] = yp[u * S];
-            }
-        for (int64_t t0 = 0; t0 < T; t0 += NB) {
-#pragma unroll
-            for (int u = 0; u < NB; ++u) {
-                const int64_t t = t0 + u;
-                if (t < T) {
-                    const int64_t tp = t + NB - 1;
-                    if (tp < T) {
-                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                        yb[(u + NB - 1) % NB] = yp[tp * S];
-                    }
-                    double p[C];
-#pragma unroll
-                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
-                    const double qq = ocx_total<C, P, false>(p, lane);
-                    comp += 0.5 * fabs(qq - yb[u]);
-                }
-            }
-        }
+            for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
+            const double qq = ocx_total<C, P, false>(p, lane);
+            comp += 0.5 * fabs(qq - yb[u]);
+        });
     }
     if (__ballot(closed) != 0) {
         double p[C];
@@ -185,8 +154,9 @@ template <int C, int P>
 hipError_t launch_pipe_cp(const ocx_layout* L, const double* zt, const double* yt, int ftl,
                           double eta0, double* reg, double* cum, double* comp, int* closed_out,
                           int onepass, hipStream_t st) {
-    // z_{t+1} must be in the ring a step ahead: at least three steps in flight
-    constexpr int NB = nb_for(C, P) < 3 ? 3 : nb_for(C, P);
+    // z_{t+1} must be in the ring a step ahead, and the late loads (ocx_ring_loop) keep
+    // NB-2 steps in flight: one slot more than the plain kernel's ring
+    constexpr int NB = nb_for(C, P) + 1 < 4 ? 4 : nb_for(C, P) + 1;
     hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB>), ocx_grid(L->G, ocx_block_waves(L->G)),
                        dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->G, ftl, eta0,
                        reg, cum, comp, closed_out, onepass);
@@ -198,19 +168,20 @@ hipError_t launch_pipe_c(const ocx_layout* L, const double* zt, const double* yt
                          double eta0, double* reg, double* cum, double* comp, int* closed_out,
                          int onepass, hipStream_t st) {
     switch (L->P) {
-        case 2: return launch_pipe_cp<C, 2>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
-        case 4: return launch_pipe_cp<C, 4>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 8: return launch_pipe_cp<C, 8>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 16: return launch_pipe_cp<C, 16>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 32: return launch_pipe_cp<C, 32>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
-        case 64: return launch_pipe_cp<C, 64>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         default: return hipErrorInvalidValue;
     }
 }
 }  // namespace
 
+// The pipelined step pays where one wave's step latency sets the batch time: the few-wave
+// butterfly layouts OCX_LANES_BEST chooses (8 x 8, 16 x 4 at d = 64; 16 x 16; 32 x 32 at
+// d = 1024) and their neighbours.  Other butterfly layouts keep the plain kernel.
 bool ocx_pipe_supported(const ocx_layout* L) {
-    return !L->chain && L->P >= 2 && L->C <= 32;
+    return !L->chain && (L->P == 8 || L->P == 16 || L->P == 32) &&
+           (L->C == 4 || L->C == 8 || L->C == 16 || L->C == 32);
 }
 
 hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const double* yt, int ftl,
@@ -218,13 +189,9 @@ hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const doub
                                int* closed_out, int onepass, hipStream_t st) {
     if (L->G == 0) return hipSuccess;
     switch (L->C) {
-        case 2: return launch_pipe_c<2>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 4: return launch_pipe_c<4>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
-        case 6: return launch_pipe_c<6>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 8: return launch_pipe_c<8>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
-        case 12: return launch_pipe_c<12>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 16: return launch_pipe_c<16>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
-        case 24: return launch_pipe_c<24>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         case 32: return launch_pipe_c<32>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         default: return hipErrorInvalidValue;
     }

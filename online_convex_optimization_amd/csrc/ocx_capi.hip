@@ -694,6 +694,76 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
     return OCX_OK;
 }
 
+int ocx_dev_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                             int norm, int all_prefixes, double* actions, double* obj, double* gap,
+                             double* step_loss, int32_t* info, void* stream) {
+    if (B < 0 || T < 0 || d < 1) return fail(OCX_E_INVALID, "need B >= 0, T >= 0, d >= 1");
+    if (d > OCX_EXACT_BALL_MAX_D)
+        return fail(OCX_E_UNSUPPORTED, "the general exact-FTL solver takes d <= " +
+                                           std::to_string(OCX_EXACT_BALL_MAX_D));
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
+    if (B == 0) return OCX_OK;
+    if ((T > 0 && (!z || !y)) || !actions) return fail(OCX_E_INVALID, "NULL argument");
+    OCX_HIP(ocx_launch_exact_ball(z, y, B, T, d, norm, all_prefixes, actions, obj, gap, step_loss,
+                                  info, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_dev_exact_ball_solve_tiled(const ocx_layout* L, const double* z_tiled,
+                                   const double* y_tiled, int norm, int all_prefixes,
+                                   double* actions, double* obj, double* gap, double* step_loss,
+                                   int32_t* info, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (L->d < 1) return fail(OCX_E_INVALID, "need d >= 1");
+    if (L->d > OCX_EXACT_BALL_MAX_D)
+        return fail(OCX_E_UNSUPPORTED, "the general exact-FTL solver takes d <= " +
+                                           std::to_string(OCX_EXACT_BALL_MAX_D));
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
+    if (L->B == 0) return OCX_OK;
+    if ((L->z_elems && (!z_tiled || !y_tiled)) || !actions) return fail(OCX_E_INVALID, "NULL argument");
+    OCX_HIP(ocx_launch_exact_ball_tiled(L, z_tiled, y_tiled, norm, all_prefixes, actions, obj, gap,
+                                        step_loss, info, (hipStream_t)stream));
+    return OCX_OK;
+}
+
+int ocx_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                         int norm, int all_prefixes, double* actions, double* obj, double* gap,
+                         double* step_loss, int32_t* info, int device) {
+    if (B < 0 || T < 0 || d < 1) return fail(OCX_E_INVALID, "need B >= 0, T >= 0, d >= 1");
+    if (d > OCX_EXACT_BALL_MAX_D)
+        return fail(OCX_E_UNSUPPORTED, "the general exact-FTL solver takes d <= " +
+                                           std::to_string(OCX_EXACT_BALL_MAX_D));
+    if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
+    if (B == 0) return OCX_OK;
+    if ((T > 0 && (!z || !y)) || !actions) return fail(OCX_E_INVALID, "NULL argument");
+    DevCtx* cx;
+    if (int rc = ctx_enter(device, &cx)) return rc;
+    std::lock_guard<std::mutex> lk(cx->mu);
+    hipStream_t st = cx->stream;
+    const int64_t NP = all_prefixes ? T + 1 : 1;
+    const size_t nz = (size_t)(B * T * d), ny = (size_t)(B * T), na = (size_t)(B * NP * d);
+    const size_t np = (size_t)(B * NP);
+    OCX_HIP(cx->zraw.ensure(nz * 8));
+    OCX_HIP(cx->yraw.ensure(ny * 8));
+    OCX_HIP(cx->araw.ensure(na * 8));
+    OCX_HIP(cx->out.ensure(np * 28));
+    if (nz) OCX_HIP(hipMemcpyAsync(cx->zraw.p, z, nz * 8, hipMemcpyHostToDevice, st));
+    if (ny) OCX_HIP(hipMemcpyAsync(cx->yraw.p, y, ny * 8, hipMemcpyHostToDevice, st));
+    double* o = cx->out.as<double>();
+    int32_t* inf = reinterpret_cast<int32_t*>(o + 3 * np);
+    OCX_HIP(ocx_launch_exact_ball(cx->zraw.as<double>(), cx->yraw.as<double>(), B, T, d, norm,
+                                  all_prefixes, cx->araw.as<double>(), o, o + np, o + 2 * np, inf,
+                                  st));
+    OCX_HIP(hipMemcpyAsync(actions, cx->araw.p, na * 8, hipMemcpyDeviceToHost, st));
+    if (obj) OCX_HIP(hipMemcpyAsync(obj, o, np * 8, hipMemcpyDeviceToHost, st));
+    if (gap) OCX_HIP(hipMemcpyAsync(gap, o + np, np * 8, hipMemcpyDeviceToHost, st));
+    if (step_loss)
+        OCX_HIP(hipMemcpyAsync(step_loss, o + 2 * np, np * 8, hipMemcpyDeviceToHost, st));
+    if (info) OCX_HIP(hipMemcpyAsync(info, inf, np * 4, hipMemcpyDeviceToHost, st));
+    OCX_HIP(hipStreamSynchronize(st));
+    return OCX_OK;
+}
+
 }  // extern "C"
 
 namespace {

@@ -38,6 +38,49 @@ constexpr int nb_for(int C, int P = 1, bool deep = true) {
     return C <= 8 ? ((deep && P < 32) ? OCX_NB_LE8 : 4) : (C <= 16 ? OCX_NB_16 : OCX_NB_GE32);
 }
 
+// The register-ring loop of the streaming kernels: steps t in [0, T) with NB-1 steps of
+// loads in flight.  load(slot, t) issues step t's loads into ring slot `slot`; step(u, t)
+// consumes slot u (u is a compile-time constant once the loop is unrolled).  Every full
+// block of NB steps issues its loads unconditionally — a look-ahead past the end re-reads
+// step T-1, harmless — so the compiler's s_waitcnt pass sees a fixed sequence of loads and
+// waits only for the slot about to be used.  (With the loads behind `if (t + NB - 1 < T)`
+// it could not count them, and waited at every step for nearly every load in flight,
+// including the look-ahead just issued: the ring hid no latency.)  The last block's steps
+// past T are skipped; its loads are still issued (clamped), so the count stays fixed.
+// Ring cycles per loop iteration (tuning knob): the compiler's wait at the loop header
+//  then drains the look-ahead once per OCX_RING_UNROLL * NB steps.
+#ifndef OCX_RING_UNROLL
+#define OCX_RING_UNROLL 1
+#endif
+// LATE = true issues each block step's look-ahead load after the step instead of before it
+// (NB-2 steps in flight instead of NB-1): for a step that still reads the slot the early
+// load would overwrite (ocx_alg_pipe_kernel's z_{t-1}), which otherwise makes the register
+// allocator rotate the ring with copies at the loop's back edge — and every copy of an
+// in-flight slot is a wait for its load.
+template <int NB, bool LATE = false, class Load, class Step>
+__device__ __forceinline__ void ocx_ring_loop(int64_t T, Load&& load, Step&& step) {
+    static_assert(NB >= (LATE ? 3 : 2), "a ring with at least one step in flight");
+    constexpr int BL = NB * OCX_RING_UNROLL;  // steps per loop iteration
+    if (T <= 0) return;
+#pragma unroll
+    for (int u = 0; u < NB - 1; ++u) {
+        load(u, u < T ? (int64_t)u : T - 1);
+        // keep the prologue's loads in slot order: the loop header merges this order with
+        // the back edge's, and a slot the scheduler loaded last here would be waited for
+        // as if it were the newest load on every pass (a drain once per ring cycle)
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int64_t t0 = 0; t0 < T; t0 += BL) {
+#pragma unroll
+        for (int u = 0; u < BL; ++u) {
+            const int64_t tp = t0 + u + NB - 1;
+            if (!LATE) load((u + NB - 1) % NB, tp < T ? tp : T - 1);  // unconditional: above
+            if (t0 + u < T) step(u % NB, t0 + u);  // the last block may be short
+            if (LATE) load((u + NB - 1) % NB, tp < T ? tp : T - 1);
+        }
+    }
+}
+
 template <int C>
 __device__ __forceinline__ void ocx_load_tile(ocx_d2 (&dst)[C / 2], const ocx_d2* __restrict__ p,
                                               int64_t kst) {
@@ -97,19 +140,19 @@ __device__ __forceinline__ double ocx_bcast_last(double v, int lane) {
     if constexpr (P == 1) {
         return v;
     } else if constexpr (P == 2) {
-        return ocx_dpp<0xF5>(v);  // quad_perm [1,1,3,3]
+        return ocx_dpp_all<0xF5>(v);  // quad_perm [1,1,3,3]
     } else if constexpr (P == 4) {
-        return ocx_dpp<0xFF>(v);  // quad_perm [3,3,3,3]
+        return ocx_dpp_all<0xFF>(v);  // quad_perm [3,3,3,3]
     } else if constexpr (P == 8) {
-        const double s1 = ocx_dpp<0xFF>(v);    // lanes 4-7 of the half-row: lane 7's value
-        const double s2 = ocx_dpp<0x141>(s1);  // half-row mirror: lanes 0-3 <- lanes 7-4
+        const double s1 = ocx_dpp_all<0xFF>(v);    // lanes 4-7 of the half-row: lane 7's value
+        const double s2 = ocx_dpp_all<0x141>(s1);  // half-row mirror: lanes 0-3 <- lanes 7-4
         return (lane & 4) ? s1 : s2;
     } else if constexpr (P == 16) {
         const int r = lane & 15;
-        const double s1 = ocx_dpp<0xFF>(v);    // lanes 12-15: lane 15's value
-        const double s2 = ocx_dpp<0x140>(s1);  // row mirror: lanes 0-3 <- lanes 15-12
-        const double m = r >= 12 ? s1 : s2;    // right in lanes 0-3 and 12-15
-        const double s3 = ocx_dpp<0x141>(m);   // half mirrors: 4-7 <- 3-0, 8-11 <- 15-12
+        const double s1 = ocx_dpp_all<0xFF>(v);    // lanes 12-15: lane 15's value
+        const double s2 = ocx_dpp_all<0x140>(s1);  // row mirror: lanes 0-3 <- lanes 15-12
+        const double m = r >= 12 ? s1 : s2;        // right in lanes 0-3 and 12-15
+        const double s3 = ocx_dpp_all<0x141>(m);   // half mirrors: 4-7 <- 3-0, 8-11 <- 15-12
         return (r < 4 || r >= 12) ? m : s3;
     } else if constexpr (P == 32) {
         const double lo = ocx_readlane(v, 31), hi = ocx_readlane(v, 63);

@@ -32,9 +32,11 @@ namespace {
 
 constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 
-// Float fast path of the ziggurat's wedge test (see zig_round); 0 = the double form.
+// Float fast path of the ziggurat's wedge test (see zig_round; 0 = the double form).
+// Measured no faster (d = 64, 32768 x 1e4: 71.5 vs 71.1 ms, profiles/r03_gen_ab.jsonl):
+// off by default, kept as a tuning knob.
 #ifndef OCX_GEN_WEDGE_F32
-#define OCX_GEN_WEDGE_F32 1
+#define OCX_GEN_WEDGE_F32 0
 #endif
 
 struct ZigTables {
@@ -52,12 +54,13 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
 __device__ __forceinline__ ocx_u128 rl128(ocx_u128 v, int lane) {
     return ((ocx_u128)rl64((uint64_t)(v >> 64), lane) << 64) | rl64((uint64_t)v, lane);
 }
-// lane k gets lane k+1's value (DPP wave_shl:1, a VALU move; lane 63 keeps its own, which
-// no caller reads: a rejected lane 63 is redrawn next round)
+// lane k gets lane k+1's value (DPP wave_shl:1, a VALU move; lane 63 gets 0 (bound_ctrl,
+// no copy of the old value first), which no caller reads: a rejected lane 63 is redrawn
+// next round)
 __device__ __forceinline__ uint64_t shfl_down1(uint64_t v) {
     int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
-    lo = __builtin_amdgcn_update_dpp(lo, lo, 0x130, 0xF, 0xF, false);
-    hi = __builtin_amdgcn_update_dpp(hi, hi, 0x130, 0xF, 0xF, false);
+    lo = __builtin_amdgcn_mov_dpp(lo, 0x130, 0xF, 0xF, true);
+    hi = __builtin_amdgcn_mov_dpp(hi, 0x130, 0xF, 0xF, true);
     return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 __device__ __forceinline__ double shfl_double(double v, int src) {
@@ -210,16 +213,21 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 // the stream past exactly the draws those normals consumed (NumPy random_standard_normal).
 // FULL: need == 64 is known (every round of a d = 64 row stream but the last): a rejection
 // round then appends at most 63 normals, so the need-capping tail below drops out.
-// Speculative next-round state (OCX_GEN_SPEC_NEXT, default on): the next round's
-// multiply-add is issued right after this round's, from lane 63's state, so it overlaps
-// this round's table lookup, test and parse instead of waiting behind them; a round that
-// stops short of draw 63 (a rejected lane 63, a tail draw, the last round) drops it.
+// Speculative next-round state (OCX_GEN_SPEC_NEXT): the next round's multiply-add is
+// issued right after this round's, from lane 63's state, so it could overlap this round's
+// table lookup, test and parse; a round that stops short of draw 63 (a rejected lane 63, a
+// tail draw, the last round) drops it.  Measured slower (74.9 vs 71.1 ms at d = 64,
+// 32768 x 1e4, profiles/r03_gen_ab.jsonl: the kernel is VALU-bound, not latency-bound, and
+// the extra state costs registers): off by default, kept as a tuning knob.
 #ifndef OCX_GEN_SPEC_NEXT
-#define OCX_GEN_SPEC_NEXT 1
+#define OCX_GEN_SPEC_NEXT 0
 #endif
-template <bool RING, bool FULL = false>
+// FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
+// left to the front itself): ring indices go unmasked.
+template <bool RING, bool FULL = false, bool FLAT = false>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
+    const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
 #if OCX_GEN_SPEC_NEXT
     ocx_u128 s;
     if (w.have_spec) {  // wave-uniform
@@ -247,7 +255,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #endif
     const uint64_t rej = ballot(!fast);
     if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
-        if (RING) ring[(head + (unsigned)lane) & rmask] = x;
+        if (RING) ring[(head + (unsigned)lane) & fmask] = x;
 #if OCX_GEN_SPEC_NEXT
         w.base = s63;
         w.have_spec = true;
@@ -342,13 +350,13 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         n = need;
         tail_k = -1;
     }
-    if (RING && ((emit >> lane) & 1)) ring[(head + mbcnt(emit)) & rmask] = x;
+    if (RING && ((emit >> lane) & 1)) ring[(head + mbcnt(emit)) & fmask] = x;
     if (tail_k >= 0) {
         // NumPy's tail loop, sequential from the state after the tail draw
         const ocx_u128 st = rl128(s, tail_k);
         const TailOut o = zig_tail((uint64_t)st, (uint64_t)(st >> 64), (uint64_t)w.inc,
                                    (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
-        if (RING && lane == 0) ring[(head + n) & rmask] = o.v;
+        if (RING && lane == 0) ring[(head + n) & fmask] = o.v;
         w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
 #if OCX_GEN_SPEC_NEXT
         w.have_spec = false;
@@ -482,11 +490,9 @@ constexpr int kWaveBlock = 256;
 #else
 #define OCX_GEN_STORE(v, p) __builtin_nontemporal_store((v), (p))
 #endif
-// Waves per SIMD the register allocation must allow.  For the d = 64 kernel 6 waves
-// (80 VGPRs, a few cold spills) measured 6 % faster than the unconstrained 104 VGPRs
-// (4 waves); its LDS (6 KB tables + 4 x 4 KB rings per block) also admits 6.
-// The default d = 64 form's 8 KB ring holds the LDS to four waves per SIMD, so it gets the
-// four-wave register budget (no spills); the few-stream form (LR, 4 KB ring) runs six.
+// Waves per SIMD the register allocation must allow.  The d = 64 kernels' rings (4.6 KB per
+// wave) and tables (6 KB per block) admit six waves per SIMD in LDS; the default form keeps
+// the four-wave register budget (no spills), the few-stream form (LR) asks for six.
 #ifndef OCX_GENW_MIN_WAVES
 #define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? 4 : 1))
 #else
@@ -506,6 +512,9 @@ __host__ __device__ __forceinline__ int batch_rows(int d) {
     return 1;
 }
 constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion depth <= 16
+// rows per batch of the d = 64 kernels (both forms; 8 rows use all 64 lanes for the
+// 8-accumulator sums of squares and share one sqrt/div sequence)
+constexpr int kRows64 = 8;
 
 }  // namespace
 
@@ -521,9 +530,8 @@ constexpr int kStackDoubles = 16 * sizeof(PwFrame) / 8;  // pairwise recursion d
 // squares uses all 64 lanes (8 leaves of 128, 8 accumulators each: the leaf and tree
 // order of NumPy's recursion is the 64-lane butterfly) and every store instruction
 // writes whole contiguous plane segments; DF = 0: any d.
-// LR (DF = 64 only): the low-LDS form for few-stream batches: 7 rows per epilogue batch
-// (7·64 + 63 pending normals fit 512 doubles) so the ring is 4 KB per wave and six waves
-// per SIMD fit the LDS; the default form's 8-row batches need 1024 (4 waves per SIMD).
+// LR (DF = 64 only): the few-stream form: the same rows, compiled for six waves per SIMD
+// (a register budget of 80 VGPRs, a few cold spills) where the default form keeps four.
 // RAW (DF = 0 only): rows left unclipped, for the float32 twin (ocx_twin32.hip), which
 // rounds them to float and clips them in float32 itself (algorithms.py:157-160).
 template <int MODE, int DF, bool LR = false, bool RAW = false>
@@ -583,7 +591,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     st1k.jstep = 2 * st1k.kstep;
     // rows leave the ring in batches of R: the sums of squares of a batch run side by
     // side (8 lanes per row for 8 <= d <= 128, one lane per row for d < 8)
-    const int R = LR ? 7 : batch_rows(d);
+    const int R = batch_rows(d);
     // store map for Dp <= 64: lane → (row of the pass, coordinate j), RP rows per pass
     const int RP = Dp <= 64 ? 64 / Dp : 1;
     const int jl = Dp <= 64 ? lane % Dp : lane;
@@ -619,43 +627,47 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
 
         // ---- rows
         if constexpr (MODE == 0 && DF == 64) {
-            // d = 64: lean bookkeeping (the generic loop below spends scalar instructions on
-            // partial/ready counters every round): head − tailp normals wait in the ring, a
-            // batch of R rows leaves as soon as it is complete (at most one per round: the
-            // ring never holds more than R rows + 63), the rest after the last round
+            // d = 64, a front-moving ring of R rows + one round (kRows64 * 64 + 64 doubles):
+            // rows always start at ring[0], so no index is ever masked and every ring access
+            // is a fixed base + an immediate offset.  A batch of R rows leaves as soon as the
+            // ring holds it (at most one per round) and the <= 63 normals drawn past it then
+            // move to the front (LDS operations of a wave run in order: the batch's reads come
+            // first); the last batch may be shorter.  The batch's row scales reach the store
+            // lanes through LDS (`scl`, one broadcast read per row) instead of readlanes.
+            constexpr int RR = kRows64;
             const uint32_t total = (uint32_t)(T * 64);
             uint32_t produced = 0;
-            unsigned head = 0, tailp = 0;
+            unsigned head = 0;  // normals in the ring
             int64_t t = 0;
+            double* scl = ring + RR * 64 + 64;  // the batch's row scales
             while (produced < total) {
                 const uint32_t left = total - produced;
                 const int n = left >= 64u
-                                  ? zig_round<true, true>(w, 64, tb, ring, rmask, head, lane)
-                                  : zig_round<true>(w, (int)left, tb, ring, rmask, head, lane);
+                                  ? zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane)
+                                  : zig_round<true, false, true>(w, (int)left, tb, ring, 0, head,
+                                                                 lane);
                 produced += (uint32_t)n;
                 head += (unsigned)n;
-                const unsigned pending = head - tailp;
-                if (pending >= (unsigned)(R * 64) || (produced == total && pending > 0)) {
-                    const int nrows = (int)(pending >> 6) < R ? (int)(pending >> 6) : R;
+                if (head >= (unsigned)(RR * 64) || (produced == total && head > 0)) {
+                    const int nrows = (int)(head >> 6) < RR ? (int)(head >> 6) : RR;
                     // lanes 8r..8r+7: row r's NumPy pairwise sum of squares, its clip scale
-                    const double ss =
-                        leaf_sumsq<64>(ring, rmask, tailp + (unsigned)((lane >> 3) * 64), 64, lane);
+                    const double ss = leaf_sumsq<64>(ring, -1, (unsigned)((lane >> 3) * 64), 64, lane);
                     const double nrm = sqrt(ss);
                     const double sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
+                    scl[lane >> 3] = sc;  // the 8 lanes of a row write the same value
                     double* zp = zt + zoff + t * 128;
-                    // lane j stores coordinate j of each row: the default form's batches
-                    // start at multiples of 512 of its 1024 ring (one base, immediate
-                    // offsets); the low-LDS form's 7-row batches wrap the 512 ring
-                    const unsigned base = tailp & (unsigned)rmask;
-                    for (int r = 0; r < nrows; ++r) {
-                        const double scr = __hiloint2double(
-                            __builtin_amdgcn_readlane(__double2hiint(sc), r * 8),
-                            __builtin_amdgcn_readlane(__double2loint(sc), r * 8));
-                        const unsigned ro = LR ? ((tailp + 64u * (unsigned)r) & (unsigned)rmask)
-                                               : base + 64u * (unsigned)r;
-                        OCX_GEN_STORE(ring[ro + (unsigned)lane] * scr, zp + r * 128);
+                    // lane j stores coordinate j of each row
+                    if (nrows == RR) {
+#pragma unroll
+                        for (int r = 0; r < RR; ++r)
+                            OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
+                    } else {
+                        for (int r = 0; r < nrows; ++r)
+                            OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
                     }
-                    tailp += (unsigned)(nrows * 64);
+                    const unsigned used = (unsigned)(nrows * 64);
+                    ring[lane] = ring[used + lane];  // the next rows' first normals to the front
+                    head -= used;
                     t += nrows;
                 }
             }
@@ -758,29 +770,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
                     sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
                 }
                 const int sc_stride = d < 8 ? 1 : 8;
-                if (DF == 64 && LR) {
-                    // 7-row batches in a 512 ring: rows of 64 never wrap, but a batch
-                    // does, so each row gets its own masked base
-                    double* zp = zt + zoff + t * 128;
-                    for (int r = 0; r < nrows; ++r) {
-                        const double scr = __hiloint2double(
-                            __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
-                            __builtin_amdgcn_readlane(__double2loint(sc), r * sc_stride));
-                        const unsigned ro = (tailp + 64u * (unsigned)r) & (unsigned)rmask;
-                        OCX_GEN_STORE(ring[ro + (unsigned)lane] * scr, zp + r * 128);
-                    }
-                } else if (DF == 64) {
-                    // whole rows of 64, never wrapping (see leaf_sumsq): lane j stores
-                    // coordinate j of each row, at immediate LDS offsets from one base
-                    const double* rp = ring + (tailp & (unsigned)rmask) + lane;
-                    double* zp = zt + zoff + t * 128;
-                    for (int r = 0; r < nrows; ++r) {
-                        const double scr = __hiloint2double(
-                            __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
-                            __builtin_amdgcn_readlane(__double2loint(sc), r * sc_stride));
-                        OCX_GEN_STORE(rp[64 * r] * scr, zp + r * 128);
-                    }
-                } else if (Dp <= 64 && d <= 128 && RP == 1) {
+                if (Dp <= 64 && d <= 128 && RP == 1) {
                     for (int r = 0; r < nrows; ++r) {
                         const double scr = __hiloint2double(
                             __builtin_amdgcn_readlane(__double2hiint(sc), r * sc_stride),
@@ -871,7 +861,7 @@ namespace {
 
 int ring_doubles(int64_t d, int DF, bool LR = false) {
     if (DF == 1024) return 1024 + 64;  // one row + the next row's first round (ocx_gen_wave_kernel)
-    if (LR) return 512;           // 7 rows + one round's normals (ocx_gen_wave_kernel, LR)
+    if (DF == 64) return kRows64 * 64 + 64 + 8;  // R rows + one round, then the R row scales
     // a full batch of rows plus one round of normals
     int rb = 128;
     while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
@@ -940,8 +930,9 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
     // the kernel counts a sequence's normals in 32 bits
     if ((MODE == 0 ? T : T_seed) * d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
     if (d == 64 && (MODE == 1 || (int64_t)P * C == 64)) {
-        // Two forms: the default (8-row batches, 4 waves per SIMD: its 8 KB ring fills the
-        // LDS) and the low-LDS one (7-row batches, 6 waves per SIMD).  Every wave takes
+        // Two forms: the default (4 waves per SIMD's register budget) and the few-stream one
+        // (6 waves per SIMD; round 2 measured these with a 7-row, 4 KB ring for the latter
+        // and an 8 KB ring for the former: both now share the 4.6 KB ring).  Every wave takes
         // ceil(streams / slots) whole streams, so a form's makespan is that count times the
         // waves of its busiest SIMD; the low-LDS form wins where that is smaller, or equal
         // within the ~6 % its extra waves buy per stream when it really runs more waves per

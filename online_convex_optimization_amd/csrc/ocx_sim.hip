@@ -73,25 +73,14 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
 
     ocx_d2 zb[NB][K];
     double yb[NB];
-#pragma unroll
-    for (int u = 0; u < NB - 1; ++u)
-        if (u < T) {
-            ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
-            yb[u] = yp[u * S];
-        }
+    auto load = [&](int slot, int64_t tl) {
+        ocx_load_tile<C>(zb[slot], zp + tl * tstride, kst);
+        yb[slot] = yp[tl * S];
+    };
 
     double cum = 0.0;
     OcxScaleTable sct;  // FTRL scales, 64 steps at a time (long chains)
-    for (int64_t t0 = 0; t0 < T; t0 += NB) {
-#pragma unroll
-        for (int u = 0; u < NB; ++u) {
-            const int64_t t = t0 + u;
-            if (t < T) {
-                const int64_t tp = t + NB - 1;
-                if (tp < T) {
-                    ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                    yb[(u + NB - 1) % NB] = yp[tp * S];
-                }
+    ocx_ring_loop<NB>(T, load, [&](int u, int64_t t) {
                 double x[C];
                 double q;  // :105
                 if (!ftl) {
@@ -138,9 +127,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 }
 #pragma unroll
                 for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);  // gq*z is exact
-            }
-        }
-    }
+    });
 
     // ---- closed-form comparator (onepass) ----
     // For rows with ||z_t|| <= 1 (the g(T) sampler's clipped rows; certified per row in
@@ -189,30 +176,13 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     } else if constexpr (CHAIN && P >= OCX_CHAIN_WIDE_P && P <= 16 && C <= 16) {
         comp = ocx_comp_pass2<C, P, CHAIN, (C <= 8 ? OCX_NB_PASS2 : 4)>(zp, yp, T, kst, S, xs, 0.0, lane);
     } else {
+        ocx_ring_loop<NB>(T, load, [&](int u, int64_t) {
+            double p[C];
 #pragma unroll
-        for (int u = 0; u < NB - 1; ++u)
-            if (u < T) {
-                ocx_load_tile<C>(zb[u], zp + u * tstride, kst);
-                yb[u] = yp[u * S];
-            }
-        for (int64_t t0 = 0; t0 < T; t0 += NB) {
-#pragma unroll
-            for (int u = 0; u < NB; ++u) {
-                const int64_t t = t0 + u;
-                if (t < T) {
-                    const int64_t tp = t + NB - 1;
-                    if (tp < T) {
-                        ocx_load_tile<C>(zb[(u + NB - 1) % NB], zp + tp * tstride, kst);
-                        yb[(u + NB - 1) % NB] = yp[tp * S];
-                    }
-                    double p[C];
-#pragma unroll
-                    for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
-                    const double q = ocx_total_last<C, P, CHAIN>(p, lane);
-                    comp += 0.5 * fabs(q - yb[u]);
-                }
-            }
-        }
+            for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
+            const double q = ocx_total_last<C, P, CHAIN>(p, lane);
+            comp += 0.5 * fabs(q - yb[u]);
+        });
         comp = ocx_comp_lane_value<P, CHAIN>(comp, lane);
     }
     if (__ballot(closed) != 0) {  // wave-uniform: the sum below crosses lanes

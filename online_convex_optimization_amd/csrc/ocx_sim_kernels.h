@@ -77,3 +77,17 @@ hipError_t ocx_launch_pack32(const ocx_layout* L, const float* z, const float* y
 // z [B][T][d] and y [B][T] row-major, x [B][d]; absr scratch [B][T]
 hipError_t ocx_launch_comp_blas(const double* z, const double* y, const double* x, int64_t B,
                                 int64_t T, int64_t d, double* absr, double* comp, hipStream_t st);
+// The general exact-FTL comparator (ocx_exact_ball.hip): z [B][T][d], y [B][T] row-major;
+// problems (b, n) for n = T … T-NP+1 (NP = all_prefixes ? T+1 : 1); actions [B][NP][d],
+// obj / gap [B][NP] and info [B][NP] (Newton steps, negative at the iteration cap).
+// d in 1..10.
+// step_loss [B][NP] (nullable): ½|z_n·x_n − y_n|, the loss FTL pays at step n with the
+// prefix-n action (0 for n = T).  The tiled form reads z / y in L's layout.
+hipError_t ocx_launch_exact_ball(const double* z, const double* y, int64_t B, int64_t T,
+                                 int64_t d, int norm, int all_prefixes, double* actions,
+                                 double* obj, double* gap, double* step_loss, int32_t* info,
+                                 hipStream_t st);
+hipError_t ocx_launch_exact_ball_tiled(const ocx_layout* L, const double* zt, const double* yt,
+                                       int norm, int all_prefixes, double* actions, double* obj,
+                                       double* gap, double* step_loss, int32_t* info,
+                                       hipStream_t st);

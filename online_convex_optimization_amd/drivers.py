@@ -183,9 +183,10 @@ EXACT_ALGOS = ("FTRL", "FTL (exact)")
 
 def exact_case_regrets(title: str, T: int, *, runs: int, replicates: int, base_seed: int = 0,
                        d: int = 5, p: float = 0.10, block_len: int = 20, lanes_per_seq: int = 1,
-                       device: int = 0) -> Dict[str, np.ndarray]:
+                       device: int = 0, norm: str = "l2") -> Dict[str, np.ndarray]:
     """exact_ftl_driver.py:157-186 for every (run, rep) of one case and T on device:
-    exact FTL prefix actions (closed form, l2) replayed → "FTL (exact)" regret; FTRL
+    exact FTL prefix actions over the ``norm`` ball (ExperimentConfig.norm, :46; closed
+    form in its regime, else the general solver) replayed → "FTL (exact)" regret; FTRL
     (eta0 = sqrt 2) against actions[T] → "FTRL" regret."""
     import torch
     family, stream0 = CASE_FAMILIES[title]
@@ -195,28 +196,28 @@ def exact_case_regrets(title: str, T: int, *, runs: int, replicates: int, base_s
     rep_idx = np.tile(np.arange(replicates), runs)
     db.generate_family(family, base_seed + 2025 * (run_idx + 1), stream0 + rep_idx, p=p,
                        block_len=block_len)
-    return _exact_pair(db, B, d, torch)
+    return _exact_pair(db, B, d, torch, norm)
 
 
-def _exact_pair(db, B, d, torch) -> Dict[str, np.ndarray]:
+def _exact_pair(db, B, d, torch, norm: str = "l2") -> Dict[str, np.ndarray]:
     """Both regrets of exact_ftl_driver.py:169-184 in one read of the batch
-    (ocx_dev_ftrl_vs_exact): FTRL and exact FTL against the exact comparator actions[T]."""
-    regime = db.ftrl_vs_exact(SQRT2)
-    if not bool(regime[:B].all()):
-        raise NotImplementedError("a sequence left the exact-FTL closed form's regime")
+    (ocx_dev_ftrl_vs_exact): FTRL and exact FTL against the exact comparator actions[T];
+    sequences outside the closed form's regime take the general solver."""
+    db.ftrl_vs_exact_general(SQRT2, norm=norm)
     ftrl = db.cum - db.comp
     ftl = db.cum_exact - db.comp
     return {"FTRL": ftrl[:B].cpu().numpy(), "FTL (exact)": ftl[:B].cpu().numpy()}
 
 
 def exact_evaluate_stream_with_stats(title: str, T_grid: Sequence[int], *, runs: int,
-                                     replicates: int, base_seed: int = 0, device: int = 0) -> Stats:
+                                     replicates: int, base_seed: int = 0, device: int = 0,
+                                     norm: str = "l2") -> Stats:
     """exact_ftl_driver.py:120-206 for the CASES entry ``title``."""
     by_T = {k: [[] for _ in range(len(T_grid))] for k in EXACT_ALGOS}
     per_T = []
     for T in T_grid:
         r = exact_case_regrets(title, int(T), runs=runs, replicates=replicates,
-                               base_seed=base_seed, device=device)
+                               base_seed=base_seed, device=device, norm=norm)
         per_T.append({k: v.reshape(runs, replicates) for k, v in r.items()})
     for run in range(runs):
         for ti in range(len(T_grid)):
@@ -234,8 +235,8 @@ def exact_evaluate_stream_with_stats(title: str, T_grid: Sequence[int], *, runs:
 
 
 def exact_empirical_worst_case_thresholds(T_grid: Sequence[int], *, runs: int = 200,
-                                          base_seed: int = 0, d: int = 5,
-                                          device: int = 0) -> Dict[int, float]:
+                                          base_seed: int = 0, d: int = 5, device: int = 0,
+                                          norm: str = "l2") -> Dict[int, float]:
     """exact_ftl_driver.py:64-117: max over runs of FTRL's regret against the exact
     comparator, on the g(T) adversary regenerated on device."""
     import torch
@@ -244,19 +245,20 @@ def exact_empirical_worst_case_thresholds(T_grid: Sequence[int], *, runs: int = 
         T = int(T)
         db = engine.DeviceBatch(runs, T, d, lanes_per_seq=1, device=device)
         db.generate_gT(base_seed, 0)
-        r = _exact_pair(db, runs, d, torch)["FTRL"]
+        r = _exact_pair(db, runs, d, torch, norm)["FTRL"]
         g[T] = engine.max_regret(r)
     return g
 
 
 def exact_ftl_driver_main(T_grid: Optional[Sequence[int]] = None, *, g_runs: int = 200,
-                          base_seed: int = 0, device: int = 0):
-    """exact_ftl_driver.py:268-293 minus the figures: (g_emp, stats_by_case)."""
+                          base_seed: int = 0, device: int = 0, norm: str = "l2"):
+    """exact_ftl_driver.py:268-293 minus the figures: (g_emp, stats_by_case); ``norm`` is
+    ExperimentConfig.norm (:46)."""
     T_grid = list(range(100, 1100, 100)) if T_grid is None else [int(t) for t in T_grid]
     g = exact_empirical_worst_case_thresholds(T_grid, runs=g_runs, base_seed=base_seed,
-                                              device=device)
+                                              device=device, norm=norm)
     stats = {t: exact_evaluate_stream_with_stats(t, T_grid, runs=RUNS_BY_TITLE.get(t, 1),
                                                  replicates=REPLICATES_BY_TITLE.get(t, 1),
-                                                 base_seed=base_seed, device=device)
+                                                 base_seed=base_seed, device=device, norm=norm)
              for t in CASE_FAMILIES}
     return g, stats

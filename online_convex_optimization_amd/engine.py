@@ -109,7 +109,6 @@ def replay_batch(z, y, actions, *, device: int = 0):
 
 
 NORMS = {"l2": 0, "l1": 1, "linf": 2}  # the ball of exact FTL (exact_ftl.py:83-105)
-_DUAL = {"l2": "||z_t||_2 <= 1", "l1": "max_j |z_tj| <= 1", "linf": "sum_j |z_tj| <= 1"}
 
 
 def _norm_code(norm: str) -> int:
@@ -118,13 +117,44 @@ def _norm_code(norm: str) -> int:
     return NORMS[norm]
 
 
-def _reject_out_of_regime(ok: np.ndarray, norm: str = "l2") -> None:
-    if not ok.all():
-        bad = int(np.flatnonzero(~ok)[0])
-        raise NotImplementedError(
-            f"sequence {bad} is outside the closed form's regime for the {norm} ball (needs "
-            f"{_DUAL.get(norm, norm)} and y_t = ±1); the general exact-FTL SOCP/LP is out "
-            "of scope")
+def exact_ball_solve(z, y, *, norm: str = "l2", all_prefixes: bool = True, device: int = 0):
+    """The general exact-FTL solver (include/ocx.h, ocx_exact_ball_solve): ExactFTLNoClip's
+    problem min ½Σ_{i<n}|z_i·x − y_i| over the unit ``norm`` ball (exact_ftl.py:83-105) for
+    any rows and labels, on the GPU by a log-barrier path.  Problems are every prefix
+    n = 0..T of each sequence (``all_prefixes``) or n = T only.
+
+    Returns a dict of arrays over [B, NP] (NP = T+1 or 1): ``actions`` [B, NP, d]
+    (actions[:, n] the prefix-n minimiser, as compute_prefix_actions returns), ``obj``
+    (½Σ|r| at it), ``gap`` (a certified bound on obj − optimum), ``step_loss`` (½|z_n·x_n −
+    y_n|, 0 at n = T) and ``info`` (Newton steps, negative where the cap ended a solve)."""
+    code = _norm_code(norm)
+    z = _f64(z)
+    y = _f64(y)
+    B, T, d = _check_zy(z, y)
+    if d > _lib.OCX_EXACT_BALL_MAX_D:
+        raise NotImplementedError(f"the general exact-FTL solver takes d <= "
+                                  f"{_lib.OCX_EXACT_BALL_MAX_D} (got {d})")
+    NP = T + 1 if all_prefixes else 1
+    out = {"actions": np.zeros((B, NP, d)), "obj": np.zeros((B, NP)), "gap": np.zeros((B, NP)),
+           "step_loss": np.zeros((B, NP)), "info": np.zeros((B, NP), dtype=np.int32)}
+    _lib.call("ocx_exact_ball_solve", ptr(z), ptr(y), B, T, d, code, int(bool(all_prefixes)),
+              ptr(out["actions"]), ptr(out["obj"]), ptr(out["gap"]), ptr(out["step_loss"]),
+              out["info"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(device))
+    return out
+
+
+def _general_fill(z, y, ok: np.ndarray, norm: str, device: int):
+    """Sequences outside the closed form's regime, solved by the general solver: (their
+    indices, exact_ball_solve over all prefixes, exact FTL's cumulative loss Σ_n step_loss in
+    step order, the comparator loss obj[:, T]); None when every sequence is in the regime."""
+    bad = np.flatnonzero(~ok)
+    if bad.size == 0:
+        return None
+    T = z.shape[1]
+    res = exact_ball_solve(z[bad], y[bad], norm=norm, all_prefixes=True, device=device)
+    sl = res["step_loss"][:, :T]
+    cum = np.cumsum(sl, axis=1)[:, -1] if T > 0 else np.zeros(bad.size)  # sequential order
+    return bad, res, cum, res["obj"][:, T]
 
 
 def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, device: int = 0,
@@ -135,8 +165,9 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, 
     (include/ocx.h, ocx_ftl_exact_batch).
 
     Returns (cum_loss [B], comp_loss [B], comparator actions[T] [B, d], in_regime [B]);
-    with ``check_regime`` a sequence outside the regime raises NotImplementedError (the
-    general SOCP/LP is out of scope: cvxpy is absent and its results are unpinned)."""
+    with ``check_regime`` the sequences outside the regime are solved by the general solver
+    (exact_ball_solve, d <= 10) — their numbers are the SOCP / LP's; without it they keep the
+    closed form's (not the solution there: callers must reject them)."""
     code = _norm_code(norm)
     z = _f64(z)
     y = _f64(y)
@@ -150,7 +181,10 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, 
               int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok, norm)
+        g = _general_fill(z, y, ok, norm, device)
+        if g is not None:
+            bad, res, gcum, gcomp = g
+            cum[bad], comp[bad], act[bad] = gcum, gcomp, res["actions"][:, T]
     return cum, comp, act, ok
 
 
@@ -160,8 +194,8 @@ def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LAN
     (include/ocx.h, ocx_ftl_prefix_actions_batch): actions [B, T+1, d] with actions[:, t]
     the exact FTL solution of the first t rows, in the closed form of ftl_exact_batch.
 
-    Returns (actions, in_regime [B]); with ``check_regime`` a sequence outside the regime
-    raises NotImplementedError."""
+    Returns (actions, in_regime [B]); with ``check_regime`` the sequences outside the regime
+    get the general solver's actions (exact_ball_solve)."""
     code = _norm_code(norm)
     z = _f64(z)
     y = _f64(y)
@@ -172,7 +206,9 @@ def ftl_prefix_actions_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LAN
               rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok, norm)
+        g = _general_fill(z, y, ok, norm, device)
+        if g is not None:
+            act[g[0]] = g[1]["actions"]
     return act, ok
 
 
@@ -185,7 +221,9 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, norm: str = "l2",
     Returns a dict of [B] arrays: ``ftrl`` and ``exact`` regrets, ``cum_ftrl``,
     ``cum_exact``, ``comp`` (the loss of actions[T], shared by both), ``action``
     [B, d], ``in_regime``; with ``with_ftl_comparator`` also ``comp_ftl``, the loss of
-    FTL(theta_ftrl) (the comparator simulate_alg itself uses)."""
+    FTL(theta_ftrl) (the comparator simulate_alg itself uses).  With ``check_regime`` the
+    exact side of sequences outside the closed form's regime comes from the general solver
+    (exact_ball_solve), as in ftl_exact_batch."""
     z = _f64(z)
     y = _f64(y)
     B, T, d = _check_zy(z, y)
@@ -198,7 +236,10 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, norm: str = "l2",
               int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
     if check_regime:
-        _reject_out_of_regime(ok, norm)
+        g = _general_fill(z, y, ok, norm, device)
+        if g is not None:
+            bad, res, gcum, gcomp = g
+            ce[bad], cmp_e[bad], act[bad] = gcum, gcomp, res["actions"][:, T]
     out = {"ftrl": cr - cmp_e, "exact": ce - cmp_e, "cum_ftrl": cr, "cum_exact": ce,
            "comp": cmp_e, "action": act, "in_regime": ok}
     if with_ftl_comparator:
@@ -553,6 +594,48 @@ class DeviceBatch:
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
                   cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
                   _norm_code(norm), flags, self._sp)
+        return regime
+
+    def exact_general(self, norm: str = "l2", all_prefixes: bool = True):
+        """The general exact-FTL solver (exact_ball_solve) on the resident batch
+        (ocx_dev_exact_ball_solve_tiled, d <= 10): a dict of device tensors ``actions``
+        [B, NP, d], ``obj``, ``gap``, ``step_loss`` [B, NP] and ``info`` (int32), NP = T+1
+        or 1 (async on self.stream)."""
+        torch = self.torch
+        B, T, d = self.L.B, self.L.T, self.L.d
+        if d > _lib.OCX_EXACT_BALL_MAX_D:
+            raise NotImplementedError(f"the general exact-FTL solver takes d <= "
+                                      f"{_lib.OCX_EXACT_BALL_MAX_D} (got {d})")
+        NP = T + 1 if all_prefixes else 1
+        with self._on_stream():
+            out = {"actions": torch.zeros((max(B, 1), NP, d), dtype=torch.float64,
+                                          device=self.device)}
+            for k in ("obj", "gap", "step_loss"):
+                out[k] = torch.zeros((max(B, 1), NP), dtype=torch.float64, device=self.device)
+            out["info"] = torch.zeros((max(B, 1), NP), dtype=torch.int32, device=self.device)
+        _lib.call("ocx_dev_exact_ball_solve_tiled", self._lp(), self.z.data_ptr(),
+                  self.y.data_ptr(), _norm_code(norm), int(bool(all_prefixes)),
+                  out["actions"].data_ptr(), out["obj"].data_ptr(), out["gap"].data_ptr(),
+                  out["step_loss"].data_ptr(), out["info"].data_ptr(), self._sp)
+        return out
+
+    def ftrl_vs_exact_general(self, eta0: float = SQRT2, norm: str = "l2"):
+        """ftrl_vs_exact with every sequence's exact side valid: the closed form where the
+        kernel finds the regime, the general solver (exact_general) elsewhere.  Leaves
+        self.cum (FTRL), self.cum_exact and self.comp as ftrl_vs_exact does; returns the
+        regime flags.  Synchronises once (to see whether any sequence left the regime)."""
+        torch = self.torch
+        regime = self.ftrl_vs_exact(eta0, norm=norm)
+        B, T = self.L.B, self.L.T
+        with self._on_stream():
+            ok = regime[:B].bool()
+            if bool(ok.all().item()):
+                return regime
+            g = self.exact_general(norm)
+            gcum = g["step_loss"][:B, :T].sum(dim=1)
+            gcomp = g["obj"][:B, T]
+            self.cum_exact[:B] = torch.where(ok, self.cum_exact[:B], gcum)
+            self.comp[:B] = torch.where(ok, self.comp[:B], gcomp)
         return regime
 
     def max_regret(self, out=None):

@@ -96,12 +96,18 @@ def test_exact_driver_loop_body(ef):
             assert ftrl.regret == O.simulate_alg_full(z_arr, y_arr, 0, SQ2, comparator=a)[1] - cb
 
 
-def test_out_of_regime_rejected(ef):
+def test_out_of_regime_general(ef):
+    """Outside the closed form's regime the drop-in takes the general solver (round 2
+    raised NotImplementedError; tests/test_gpu_exact_general.py checks the answers); only
+    d > 10 there is unsupported."""
     z, y, _ = O.random_iid_sample(2025, 50, 0)
+    a = ef.compute_prefix_actions(ef.ExactFTLNoClip(5, 50), 3.0 * z, y)
+    assert a.shape == (51, 5) and np.all(np.linalg.norm(a, axis=1) <= 1.0 + 1e-12)
+    x = ef.ExactFTLNoClip(5, 50).solve_prefix_from_full(z, 0.5 * y, 50)
+    assert np.linalg.norm(x) <= 1.0 + 1e-12
+    zz = 3.0 * np.random.default_rng(0).standard_normal((20, 11))
     with pytest.raises(NotImplementedError):
-        ef.compute_prefix_actions(ef.ExactFTLNoClip(5, 50), 3.0 * z, y)
-    with pytest.raises(NotImplementedError):
-        ef.ExactFTLNoClip(5, 50).solve_prefix_from_full(z, 0.5 * y, 50)
+        ef.compute_prefix_actions(ef.ExactFTLNoClip(11, 20), zz, np.ones(20))
 
 
 def test_prefix_actions_batch_lane_splits(ef):
@@ -170,10 +176,11 @@ def test_poly_exact_ftl_matches_oracle(ef, norm):
                                                  O.comparator_loss_blas_order(z[0], y[0], ref[0][4][-1]))
 
 
-def test_poly_out_of_regime_rejected(ef):
+def test_poly_out_of_regime_general(ef):
+    from tests._scipy_solvers import lp_solve
     z, y, _ = O.random_iid_sample(2025, 50, 0)     # ||z_t||_2 <= 1: inside l1, not linf
     ef.run_ftl_exact(z, y, norm="l1")
-    with pytest.raises(NotImplementedError):
-        ef.run_ftl_exact(z, y, norm="linf")
-    with pytest.raises(NotImplementedError):
-        ef.run_ftl_exact(3.0 * z, y, norm="l1")
+    for zz, norm in ((z, "linf"), (3.0 * z, "l1")):  # the general solver (LP optimum)
+        r = ef.run_ftl_exact(zz, y, norm=norm)
+        _, f = lp_solve(zz, y, norm)
+        assert abs(r.comp_loss - f) <= 1e-8 * (1.0 + f)

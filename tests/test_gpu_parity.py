@@ -262,8 +262,8 @@ def test_errors_are_loud(ocx):
     fa = ocx["fa"]
     with pytest.raises(ValueError):
         fa.simulate_alg(np.zeros((4, 2)), np.zeros(3), 0, 1.0)
-    with pytest.raises(NotImplementedError):
-        ocx["ef"].run_ftrl(np.zeros((4, 2)), np.zeros(4))
+    with pytest.raises(NotImplementedError):   # labels 0: the general solver, d > 10
+        ocx["ef"].run_ftrl(np.zeros((4, 11)), np.zeros(4))
 
 
 # ------------------------------------------------------------------ full-size properties
@@ -484,8 +484,11 @@ def test_ftl_exact_matches_oracle(ocx):
     ref = O.simulate_alg_full(z[1], y[1], 0, SQ2, comparator=a1)
     c1 = O.comparator_loss_blas_order(z[1], y[1], a1)
     assert (rr.regret, rr.cum_loss, rr.comp_loss) == (ref[1] - c1, ref[1], c1)
-    with pytest.raises(NotImplementedError):
-        ef.run_ftl_exact(2.0 * z[0], y[0])
+    # outside the regime: the general solver's actions, replayed (tests/test_gpu_exact_general.py)
+    g = eng.exact_ball_solve(2.0 * z[:1], y[:1])
+    r2 = ef.run_ftl_exact(2.0 * z[0], y[0])
+    assert np.array_equal(r2.x_last, g["actions"][0, T])
+    assert r2.cum_loss == np.cumsum(g["step_loss"][0, :T])[-1]
 
 
 @pytest.mark.parametrize("B,T,d", [(21, 300, 7), (33, 257, 64), (5, 40, 1024), (4, 0, 3),
@@ -514,9 +517,11 @@ def test_ftrl_vs_exact_fused_matches_oracle(ocx, B, T, d):
                 assert got == want and np.array_equal(r["action"][b], ra), (P, b)
             else:  # butterfly sums + closed-form comparator losses
                 assert close_closed(got, want, T) and close(r["action"][b], ra), (P, b)
-    if B and T:
-        with pytest.raises(NotImplementedError):
-            eng.ftrl_vs_exact_batch(2.0 * z, y, SQ2)
+    if B and T and d <= 10:   # outside the regime: the general solver's comparator
+        r2 = eng.ftrl_vs_exact_batch(2.0 * z, y, SQ2)
+        assert not r2["in_regime"].any()
+        g = eng.exact_ball_solve(2.0 * z, y, all_prefixes=False)
+        assert np.array_equal(r2["action"], g["actions"][:, 0])
 
 
 def test_exact_driver_matches_oracle(ocx):
