@@ -30,52 +30,78 @@
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
-template <int C, int P, int NB>
+template <int C, int P, int NB, bool FTL>
 __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
-    int64_t G, int ftl, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
+    int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass) {
-    static_assert(P >= 2 && NB >= 2, "butterfly layouts, a ring holding z_{t+1}");
+    static_assert(P >= 2 && NB >= 4, "butterfly layouts, a ring holding z_{t-1} .. z_{t+1}");
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = ocx_wave_id();
+    // wave-uniform, provably (readfirstlane): the tile bases live in SGPRs and every load
+    // is an SGPR base + the lane's constant offset, with no per-load address arithmetic
+    const int64_t g = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_wave_id());
     if (g >= G) return;
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
     const int64_t tstride = 64;  // ocx_d2 per step within a plane
-    const ocx_d2* __restrict__ zp = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride + lane;
+    const ocx_d2* __restrict__ zg = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride;
     const int64_t kst = G * T * 64;  // plane stride (pairs k)
-    const double* __restrict__ yp = yt + g * T * S + s;
+    const double* __restrict__ yg = yt + g * T * S;
     bool clean = true;  // onepass: rows in the ball, every sub-gradient −y_t/2
 
-    double th[C], zprev[C];  // θ_{t-1} (lagging one update) and z_{t-1}
+    double th[C];  // θ_{t-1} (lagging one update)
 #pragma unroll
-    for (int j = 0; j < C; ++j) th[j] = zprev[j] = 0.0;
+    for (int j = 0; j < C; ++j) th[j] = 0.0;
     double gp = 0.0;                                   // g_{t-1}
     double A = 0.0, Bz = 0.0, U = 0.0, V = 0.0, W = 0.0;  // step t's lane partials
 
+    // z_{t-1} is read where it lies, in the slot before step t's: the late loads
+    // (ocx_ring_loop<NB, true>) refill that slot only after step t.  At t = 0 that slot is
+    // the zeroed one below (g_{-1} = 0 multiplies it).
     ocx_d2 zb[NB][K];
     double yb[NB];
+#pragma unroll
+    for (int k = 0; k < K; ++k) zb[NB - 1][k] = ocx_d2{0.0, 0.0};
     auto load = [&](int slot, int64_t tl) {
-        ocx_load_tile<C>(zb[slot], zp + tl * tstride, kst);
-        yb[slot] = yp[tl * S];
+        const ocx_d2* __restrict__ row = zg + tl * tstride;  // uniform
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#if OCX_LOAD_NT
+            zb[slot][k] = __builtin_nontemporal_load(row + k * kst + lane);
+#else
+            zb[slot][k] = row[k * kst + lane];
+#endif
+        }
+        yb[slot] = yg[tl * S + s];
     };
     double cum = 0.0;
-    OcxScaleTable sct;
+    double scv = 0.0;  // −η0/√(t+1+lane) for the 64 steps from the last multiple of 64
     ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+        // every 64 steps: the FTRL scales of the next 64 steps (one per lane, one sqrt/div
+        // per lane instead of one per step) and ||θ||²'s lane part summed afresh, so the
+        // running update below drifts for at most 64 steps
+        if ((t & 63) == 0) {
+            if constexpr (!FTL) scv = -(eta0 / sqrt((double)(t + 1 + lane)));
+            double uu = 0.0;
+#pragma unroll
+            for (int j = 0; j < C; ++j) uu = __builtin_fma(th[j], th[j], uu);
+            U = uu;
+        }
         // ---- chain: g_{t-1} → z_t·θ_t, ||θ_t||² → q_t → g_t
         const double zth = __builtin_fma(gp, Bz, A);
-        const double tth = __builtin_fma(gp, __builtin_fma(gp, W, 2.0 * V), U);
+        double tth = __builtin_fma(gp, __builtin_fma(gp, W, 2.0 * V), U);
         // θ_t = θ_{t-1} + g_{t-1} z_{t-1} (exact: g is a power of two or 0)
+        const ocx_d2* zp1 = zb[(u + NB - 1) % NB];
 #pragma unroll
-        for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
+        for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, ocx_zj(zp1, j), th[j]);
         const double q_raw = ocx_seq_sum<P>(zth);
         double n_raw = ocx_seq_sum<P>(tth);
         double q;
-        if (!ftl) {
-            const double sc = ocx_ftrl_scale(sct, t + 1, eta0, lane);  // −η0/√t
+        if constexpr (!FTL) {
+            const double sc = ocx_readlane(scv, (int)(t & 63));  // −η0/√(t+1)
             const double a = sc * q_raw;
             const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
             q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
@@ -84,7 +110,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
                 double p[C];
 #pragma unroll
                 for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
-                n_raw = ocx_seq_sum<P>(ocx_lane_sum<C>(p));
+                tth = ocx_lane_sum<C>(p);
+                n_raw = ocx_seq_sum<P>(tth);
             }
             q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
         }
@@ -97,27 +124,31 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
         // ---- off the chain: step t+1's lane partials (θ_t is known, g_t is not)
         const ocx_d2* zc = zb[u];
         const ocx_d2* zn = zb[(u + 1) % NB];  // z_{t+1}, in flight since NB-2 steps
-        double w = 0.0, uu = 0.0, an = 0.0, bn = 0.0;
+        double w = 0.0, an = 0.0, bn = 0.0;
 #pragma unroll
         for (int j = 0; j < C; ++j) {
             const double zj = ocx_zj(zc, j);
             w = __builtin_fma(zj, zj, w);
-            uu = __builtin_fma(th[j], th[j], uu);
             an = __builtin_fma(ocx_zj(zn, j), th[j], an);
             bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
-            zprev[j] = zj;
         }
         if (onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
+        // (at t = T-1, zn is the clamped look-ahead: A and Bz are then never used)
         V = zth;
         W = w;
-        U = uu;
-        A = t + 1 < T ? an : 0.0;
-        Bz = t + 1 < T ? bn : 0.0;
+        U = tth;  // ||θ_t||²'s lane part, by the running update
+        A = an;
+        Bz = bn;
         gp = gq;
     });
-    // θ_T = θ_{T-1} + g_{T-1} z_{T-1}
+    // θ_T = θ_{T-1} + g_{T-1} z_{T-1} (z_{T-1} loaded again: its ring slot is not known at
+    // compile time)
+    if (T > 0) {
+        ocx_d2 zl[K];
+        ocx_load_tile<C>(zl, zg + (T - 1) * tstride + lane, kst);
 #pragma unroll
-    for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, zprev[j], th[j]);
+        for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, ocx_zj(zl, j), th[j]);
+    }
 
     // ---- comparator: closed form where certified (ocx_alg_kernel onepass), else the
     // reference's second streaming pass with x* = FTL(θ_T) (fast_algorithms.py:113-114)
@@ -154,12 +185,16 @@ template <int C, int P>
 hipError_t launch_pipe_cp(const ocx_layout* L, const double* zt, const double* yt, int ftl,
                           double eta0, double* reg, double* cum, double* comp, int* closed_out,
                           int onepass, hipStream_t st) {
-    // z_{t+1} must be in the ring a step ahead, and the late loads (ocx_ring_loop) keep
-    // NB-2 steps in flight: one slot more than the plain kernel's ring
+    // z_{t-1} .. z_{t+1} must be in the ring, and the late loads (ocx_ring_loop) keep NB-2
+    // steps in flight: one slot more than the plain kernel's ring
     constexpr int NB = nb_for(C, P) + 1 < 4 ? 4 : nb_for(C, P) + 1;
-    hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB>), ocx_grid(L->G, ocx_block_waves(L->G)),
-                       dim3(64 * ocx_block_waves(L->G)), 0, st, zt, yt, L->B, L->T, L->G, ftl, eta0,
-                       reg, cum, comp, closed_out, onepass);
+    const dim3 grid = ocx_grid(L->G, ocx_block_waves(L->G)), block(64 * ocx_block_waves(L->G));
+    if (ftl)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, true>), grid, block, 0, st, zt, yt, L->B,
+                           L->T, L->G, eta0, reg, cum, comp, closed_out, onepass);
+    else
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false>), grid, block, 0, st, zt, yt, L->B,
+                           L->T, L->G, eta0, reg, cum, comp, closed_out, onepass);
     return hipGetLastError();
 }
 

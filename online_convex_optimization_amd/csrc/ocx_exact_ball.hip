@@ -42,6 +42,7 @@ constexpr double kTolCenter = 1.0;  // λ below which μ decreases
 constexpr double kTolFinal = 1e-6;  // λ at μ_end that ends the solve
 constexpr int kFinalSteps = 6;      // or this many Newton steps at μ_end
 constexpr double kPivotFloor = 1e-13;
+constexpr double kBreakdown = 1e8;  // a Newton decrement no centred step produces
 
 // packed lower triangle, row by row: (i, j), j <= i
 __host__ __device__ constexpr int tri(int i, int j) { return i * (i + 1) / 2 + j; }
@@ -285,6 +286,14 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_exact_ball_kernel(
             }
         }
         const double lam = sqrt(lam2 > 0.0 ? lam2 : 0.0);
+        if (lam > kBreakdown) {
+            // μ has outrun fp64: with the optimal face's directions pinned only by the
+            // O(1) ball barrier and the active rows' curvature ~1/μ², the floored Cholesky
+            // returns garbage (λ ~1e19).  The iterate is the last centre, accurate to that
+            // μ (the certificate below says how well): stop there.
+            conv = true;
+            break;
+        }
         double step = lam > 0.25 ? 1.0 / (1.0 + lam) : 1.0;
         // damped Newton stays in the domain in exact arithmetic; the floored pivots do
         // not promise it, so check and halve

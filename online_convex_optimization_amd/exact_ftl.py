@@ -19,14 +19,17 @@ minimiser maximises x·S_t over the ball (engine.ftl_prefix_actions_batch / ftl_
 * Degenerate prefixes (S_t = 0, e.g. the empty prefix; ties in |S_j| for l1; zero
   coordinates of S_t for linf): the maximiser is not unique and cvxpy's choice is
   solver-dependent; the engine returns the point above (0 where S_t = 0).
-* Outside the regime the general SOCP/LP is out of scope: those calls raise
-  ``NotImplementedError``.  A caller can still pass ``comparator_action`` /
+* Outside the regime (a row beyond the dual ball, a label other than ±1 — the linf ball on
+  the reference's own rows) the GPU solves the SOCP / LP itself: a log-barrier path with a
+  certified duality gap (engine.exact_ball_solve; d <= 10, larger d raises
+  ``NotImplementedError``).  A caller can still pass ``comparator_action`` /
   ``prefix_actions`` or any solver object with the reference's methods
   (``reset_buffers`` / ``append_row`` / ``solve_prefix_from_full``).
-* Parity of the closed forms against cvxpy is **unpinned**: cvxpy is absent here and the
-  reference ships no fixture for it.  They are checked against the oracle's restatement
-  and independently against scipy (SLSQP for l2, HiGHS LPs for l1 / linf) on the CPU
-  (tests/test_exact_comparator_cpu.py).
+* Parity against cvxpy is **unpinned**: cvxpy is absent here and the reference ships no
+  fixture for it.  The closed forms are checked against the oracle's restatement and
+  independently against scipy (SLSQP for l2, HiGHS LPs for l1 / linf) on the CPU
+  (tests/test_exact_comparator_cpu.py); the general solver against the same scipy solvers
+  on the GPU (tests/test_gpu_exact_general.py).
 """
 from __future__ import annotations
 
@@ -64,12 +67,11 @@ _NORMS = ("l2", "linf", "l1")
 class ExactFTLNoClip:
     """exact_ftl.py:62-193: exact FTL over the unit norm ball, one reusable solver per
     (d, T_max) holding the current prefix in ``_Z_buf`` / ``_y_buf`` / ``_w_buf`` as the
-    reference does.  Every solve runs on the GPU in closed form (module docstring); the
-    ``solver`` / ``solver_opts`` arguments are accepted and kept for signature parity
-    (no cvxpy backend is involved).
+    reference does.  Every solve runs on the GPU — in closed form where it is exact, by the
+    general barrier solver elsewhere (module docstring); the ``solver`` / ``solver_opts``
+    arguments are accepted and kept for signature parity (no cvxpy backend is involved).
 
-    ``norm`` 'l2', 'l1' or 'linf' (closed forms, module docstring); anything else raises
-    ValueError (exact_ftl.py:101-102)."""
+    ``norm`` 'l2', 'l1' or 'linf'; anything else raises ValueError (exact_ftl.py:101-102)."""
 
     def __init__(self, d: int, T_max: int, *, norm: Literal["l2", "linf", "l1"] = "l2",
                  solver: Optional[str] = None, solver_opts: Optional[dict] = None) -> None:
@@ -87,7 +89,7 @@ class ExactFTLNoClip:
 
     # -- solves ---------------------------------------------------------------
     def _solve_length(self, z_src: np.ndarray, y_src: np.ndarray, length: int) -> np.ndarray:
-        """Exact FTL solution of the first ``length`` rows (GPU, closed form)."""
+        """Exact FTL solution of the first ``length`` rows (GPU)."""
         _, _, act, _ = _engine.ftl_exact_batch(z_src[None, :length], y_src[None, :length],
                                                norm=self.norm, lanes_per_seq=_fa.EXACT,
                                                device=_fa._DEVICE)

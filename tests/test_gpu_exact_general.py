@@ -52,7 +52,7 @@ def _check_certificate(res, ref_f, b, n):
 
 @pytest.mark.parametrize("norm", ["linf", "l1"])
 @pytest.mark.parametrize("d,clip,labels", [(5, True, "pm1"), (2, False, "pm1"), (8, True, "real"),
-                                           (10, False, "real")])
+                                           (10, False, "real"), (10, True, "pm1")])
 def test_general_lp_matches_highs(eng, norm, d, clip, labels):
     B, T = 3, 40
     z, y = _data(11 * d + (norm == "l1"), B, T, d, clip=clip, labels=labels)
@@ -60,7 +60,7 @@ def test_general_lp_matches_highs(eng, norm, d, clip, labels):
     assert res["actions"].shape == (B, T + 1, d)
     for b in range(B):
         assert np.all(res["actions"][b, 0] == 0.0)              # the empty prefix: x = 0
-        for n in (1, 2, d, d + 1, T // 2, T):
+        for n in (1, 2, 3, d // 2, d, d + 1, T // 2, T):
             x_lp, f_lp = lp_solve(z[b, :n], y[b, :n], norm)
             x = res["actions"][b, n]
             f = res["obj"][b, n]

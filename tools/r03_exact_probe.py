@@ -1,0 +1,53 @@
+"""General exact-FTL solver timing probe (round 3): ocx_dev_exact_ball_solve_tiled on the
+exact driver's shapes (d = 5, every prefix of T = 100..1000, the linf ball, on the i.i.d.
+family's clipped rows), and the exact g(T) comparator (final prefix only, 200 runs).  One
+JSON line per shape: kernel ms, problems/s, mean Newton steps, max certified gap."""
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from online_convex_optimization_amd import engine  # noqa: E402
+
+
+def time_solve(db, norm, all_prefixes, reps=3):
+    g = db.exact_general(norm, all_prefixes)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(db.stream)
+    for _ in range(reps):
+        g = db.exact_general(norm, all_prefixes)
+    ev[1].record(db.stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps, g
+
+
+def main():
+    rng = np.random.default_rng(0)
+    for B, T, d, norm, allp in ((48, 100, 5, "linf", True), (48, 1000, 5, "linf", True),
+                                (48, 1000, 5, "l1", True), (48, 1000, 5, "l2", True),
+                                (200, 1000, 5, "linf", False), (1024, 1000, 10, "linf", True)):
+        z = rng.standard_normal((B, T, d))
+        z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+        y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+        db = engine.DeviceBatch(B, T, d, lanes_per_seq=1).pack(z, y)
+        t0 = time.perf_counter()
+        ms, g = time_solve(db, norm, allp)
+        info = g["info"][:B].cpu().numpy()
+        gap = g["gap"][:B].cpu().numpy()
+        nprob = info.size
+        print(json.dumps({"B": B, "T": T, "d": d, "norm": norm, "all_prefixes": allp,
+                          "problems": int(nprob), "kernel_ms": ms,
+                          "problems_per_s": nprob / (ms * 1e-3),
+                          "newton_mean": float(np.abs(info).mean()),
+                          "capped": int((info < 0).sum()), "gap_max": float(gap.max()),
+                          "wall_s": time.perf_counter() - t0}), flush=True)
+        del db, g
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
