@@ -25,8 +25,8 @@
 // redundantly (Jacobi-scaled Cholesky, pivots floored at 1e-13 for the μ → 0
 // ill-conditioning), so the control flow stays wave-uniform.  Problems are issued longest
 // first.  A final pass certifies each answer: obj = ½Σ|r_i| and a dual bound
-// −λ·y − ||Zᵀλ||_* for two feasible duals (|λ_i| <= ½: the barrier's λ_i = r_i/(2 s_i),
-// and that one with the clearly inactive rows rounded to ±½); gap = obj − best bound >= 0
+// −λ·y − ||Zᵀλ||_* for three feasible duals (|λ_i| <= ½: the barrier's λ_i = r_i/(2 s_i),
+// that one with the clearly inactive rows rounded to ±½, and 0); gap = obj − best bound >= 0
 // bounds obj − optimum.  This is a compute kernel (≈50 passes over each prefix), not a
 // streaming one: its bound is the VALU, and the answer's accuracy (≈1e-9) is set by μ_end.
 #include "ocx_internal.h"
@@ -366,7 +366,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_exact_ball_kernel(
         na = sqrt(na);
         nb = sqrt(nb);
     }
-    const double bound = fmax(-Ya - na, -Yb - nb);
+    // λ = 0 is feasible too (bound 0): it certifies the zero-loss prefixes (n < d rows
+    // interpolated exactly) where a solve stopped early leaves the barrier's λ far off
+    const double bound = fmax(fmax(-Ya - na, -Yb - nb), 0.0);
     if (lane == 0) {
         double* xo = actions + (b * NP + slot) * D;
 #pragma unroll

@@ -134,9 +134,33 @@ __device__ __noinline__ TailOut zig_tail(uint64_t st_lo, uint64_t st_hi, uint64_
 struct WaveStream {
     ocx_u128 base, inc;
     ocx_u128 Ak, Dk;
+    ocx_u128 C64;  // inc·(A^63 + … + A + 1): the 64-draw jump's additive part (uniform)
     ocx_u128 spec;
     bool have_spec;
 };
+
+// Next round's base after a round that consumed all 64 draws: lane 63's state, which is
+// also A^64·base + C64.  OCX_GEN_SCALAR_NEXT computes it that way from the uniform base — a
+// 128-bit multiply on the scalar unit, beside the round's vector work and independent of it —
+// instead of four readlanes that wait for lane 63's vector multiply.  Bit-identical, and
+// measured slower (d = 64, 32768 x 1e4: 83.0 vs 70.5 ms, profiles/r03_gen_scalar_ab.jsonl:
+// the kernel already runs out of SGPRs, and the jump's temporaries add spills through VGPR
+// lanes): off by default, kept as a tuning knob.
+#ifndef OCX_GEN_SCALAR_NEXT
+#define OCX_GEN_SCALAR_NEXT 0
+#endif
+constexpr ocx_u128 pcg_pow(int n) {
+    ocx_u128 a = 1;
+    for (int i = 0; i < n; ++i) a = a * OCX_PCG_MULT;
+    return a;
+}
+constexpr ocx_u128 pcg_gsum(int n) {  // A^(n-1) + … + A + 1
+    ocx_u128 g = 0;
+    for (int i = 0; i < n; ++i) g = g * OCX_PCG_MULT + 1;
+    return g;
+}
+constexpr ocx_u128 kA64 = pcg_pow(64);
+constexpr ocx_u128 kG64 = pcg_gsum(64);
 
 // ---- (a * b + d) mod 2^128 with a, d per lane and b wave-uniform (SGPRs) --------------
 // Ten 32x32 partial products: six v_mad_u64_u32 (the 64-bit columns, each keeping its
@@ -205,6 +229,7 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
     w.base = rl128(g.state, 0);
     w.inc = g.inc;
     w.Dk = g.inc * Gk;
+    w.C64 = rl128(g.inc, 0) * kG64;
     w.have_spec = false;
 }
 
@@ -259,6 +284,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #if OCX_GEN_SPEC_NEXT
         w.base = s63;
         w.have_spec = true;
+#elif OCX_GEN_SCALAR_NEXT
+        w.base = w.base * kA64 + w.C64;
 #else
         w.base = rl128(s, 63);
 #endif
@@ -371,6 +398,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         w.base = rl128(s, m - 1);
         w.have_spec = false;
     }
+#elif OCX_GEN_SCALAR_NEXT
+    w.base = m == 64 ? w.base * kA64 + w.C64 : rl128(s, m - 1);
 #else
     w.base = rl128(s, m - 1);
 #endif

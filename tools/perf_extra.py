@@ -261,3 +261,9 @@ if __name__ == "__main__":
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
+        # hand everything back before the next item: the sweeps size their resident batches
+        # by the free HBM, which torch's cache and the engine's buffers would otherwise hold
+        import torch
+        from online_convex_optimization_amd import engine
+        engine.release_buffers()
+        torch.cuda.empty_cache()

@@ -9,7 +9,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from online_convex_optimization_amd import engine  # noqa: E402
 
 

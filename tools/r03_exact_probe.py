@@ -3,13 +3,14 @@ exact driver's shapes (d = 5, every prefix of T = 100..1000, the linf ball, on t
 family's clipped rows), and the exact g(T) comparator (final prefix only, 200 runs).  One
 JSON line per shape: kernel ms, problems/s, mean Newton steps, max certified gap."""
 import json
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from online_convex_optimization_amd import engine  # noqa: E402
 
 
@@ -38,12 +39,18 @@ def main():
         ms, g = time_solve(db, norm, allp)
         info = g["info"][:B].cpu().numpy()
         gap = g["gap"][:B].cpu().numpy()
+        obj = g["obj"][:B].cpu().numpy()
         nprob = info.size
+        wb, wn = np.unravel_index(int(np.argmax(gap)), gap.shape)
+        worst = {"b": int(wb), "slot": int(wn), "gap": float(gap[wb, wn]), "obj": float(obj[wb, wn]),
+                 "info": int(info[wb, wn]),
+                 "x": g["actions"][wb, wn].cpu().numpy().tolist(),
+                 "n_gap_over_1e-4": int((gap > 1e-4 * (1 + obj)).sum())}
         print(json.dumps({"B": B, "T": T, "d": d, "norm": norm, "all_prefixes": allp,
                           "problems": int(nprob), "kernel_ms": ms,
                           "problems_per_s": nprob / (ms * 1e-3),
                           "newton_mean": float(np.abs(info).mean()),
-                          "capped": int((info < 0).sum()), "gap_max": float(gap.max()),
+                          "capped": int((info < 0).sum()), "gap_max": float(gap.max()), "worst": worst,
                           "wall_s": time.perf_counter() - t0}), flush=True)
         del db, g
         torch.cuda.empty_cache()
