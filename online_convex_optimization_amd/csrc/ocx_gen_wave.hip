@@ -247,6 +247,9 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 #ifndef OCX_GEN_SPEC_NEXT
 #define OCX_GEN_SPEC_NEXT 0
 #endif
+#ifndef OCX_GEN_FAST_REJ
+#define OCX_GEN_FAST_REJ 1
+#endif
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.
 template <bool RING, bool FULL = false, bool FLAT = false>
@@ -291,6 +294,39 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #endif
         return 64;
     }
+#if OCX_GEN_FAST_REJ
+    if constexpr (FULL && !FLAT) {
+        // The common rejection round (≈3/4 of them): one rejected draw k < 63 that is not a
+        // tail draw.  Its wedge test runs on every lane (no exec-mask branch; lanes other than
+        // k compute values nobody reads), the outcome is read off two ballots, and the
+        // emission is a lane shift: lanes below k keep their slot, draw k+1 is its uniform,
+        // lanes above it move down by one (wedge accepted) or two.  The arithmetic of lane k
+        // is the general path's below, so the normals are the same; a wedge too close to
+        // call, and every other pattern, take the general path.  Bit-identical; measured
+        // (profiles/r03_gen_rej_ab.jsonl) 91.7 → 88.8 ms on the d = 1024 rows (2048 x 1e4),
+        // but 70.7 → 73.9 ms on the d = 64 form (FLAT), which keeps the general path.
+        const uint64_t zidx = ballot(idx == 0);
+        if ((rej & (rej - 1)) == 0 && (rej >> 63) == 0 && (rej & zidx) == 0) {
+            const int k = __builtin_ctzll(rej);
+            const uint64_t rn = shfl_down1(r);
+            const int i1 = idx ? idx : 1;  // lane k has idx != 0; the others any valid row
+            const double lhs = (tb.fi[i1 - 1] - tb.fi[i1]) * u53(rn) + tb.fi[i1];
+            const double e = (double)__expf((float)(-0.5 * x * x));
+            const uint64_t sure_acc = ballot(lhs < e * (1.0 - 1e-5));
+            const uint64_t sure_rej = ballot(lhs > e * (1.0 + 1e-5));
+            const uint64_t kb = 1ULL << k;
+            if ((sure_acc | sure_rej) & kb) {
+                const bool wa = (sure_acc & kb) != 0;
+                const unsigned sh = wa ? 1u : 2u;
+                const bool skip = lane == k + 1 || (!wa && lane == k);
+                if (RING && !skip)
+                    ring[(head + (unsigned)lane - (lane > k + 1 ? sh : 0u)) & fmask] = x;
+                w.base = rl128(s, 63);
+                return wa ? 63 : 62;
+            }
+        }
+    }
+#endif
     uint64_t cons = 0, wacc = 0;
     int limit = 64, tail_k = -1;
     if (rej) {
