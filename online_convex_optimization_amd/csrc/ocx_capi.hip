@@ -801,12 +801,13 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         if (dmax || regrets_on_device) OCX_HIP(hipStreamSynchronize(st));
         return OCX_OK;
     };
-    // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB): by default 95 % of
-    // what is free plus what this context already holds, at most 272 GiB (the MI355X's
-    // 288 GiB less room for everything else).  Long horizons run few-wave, latency-bound
-    // batches, so a batch's time hardly grows with its size: d = 64, T = 1e5 measured
-    // 1.62e9 timesteps/s at 192 GiB and 1.91e9 at 240 GiB (round 1); at 272 GiB a batch
-    // holds ≈5 600 sequences instead of ≈4 900.
+    // HBM budget for the z/y tiles of one batch (OCX_HBM_BUDGET_GB): by default 90 % of
+    // what is free plus what this context already holds, at most 240 GiB.  d = 64, T = 1e5
+    // measured 1.62e9 timesteps/s at 192 GiB and 1.91e9 at 240 GiB (round 1, FTRL-bound);
+    // since round 3 the generator (VALU-bound: its time grows with the streams) dominates
+    // those batches, and 272 GiB measured no faster at T = 1e5 (3.82 vs 3.80 s) and 4 %
+    // slower for configs[4] (d = 1024 batches of 3 277 put four generator waves on some
+    // SIMDs where 2 979 put three; profiles/r03_sweep_budget272.jsonl).
     int64_t budget;
     if (const char* e = std::getenv("OCX_HBM_BUDGET_GB")) {
         budget = (int64_t)(std::atof(e) * (1 << 30));
@@ -814,7 +815,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         size_t fr = 0, tot = 0;
         OCX_HIP(hipMemGetInfo(&fr, &tot));
         const double avail = (double)fr + (double)cx->zt.cap + (double)cx->yt.cap;
-        budget = std::min<int64_t>((int64_t)272 << 30, (int64_t)(0.95 * avail));
+        budget = std::min<int64_t>((int64_t)240 << 30, (int64_t)(0.9 * avail));
     }
     const int64_t kBatch = 131072;   // streams per batch of the streamed path
     // Resident batches (one generation pass) win over the streamed path (seek + two
