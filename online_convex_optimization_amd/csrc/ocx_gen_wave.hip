@@ -250,6 +250,10 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 #ifndef OCX_GEN_FAST_REJ
 #define OCX_GEN_FAST_REJ 1
 #endif
+// d = 64 row loop: an inner loop of full rounds while a whole batch is still to draw
+#ifndef OCX_GEN_INNER
+#define OCX_GEN_INNER 1
+#endif
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.
 template <bool RING, bool FULL = false, bool FLAT = false>
@@ -706,13 +710,27 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             int64_t t = 0;
             double* scl = ring + RR * 64 + 64;  // the batch's row scales
             while (produced < total) {
-                const uint32_t left = total - produced;
-                const int n = left >= 64u
-                                  ? zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane)
-                                  : zig_round<true, false, true>(w, (int)left, tb, ring, 0, head,
-                                                                 lane);
-                produced += (uint32_t)n;
-                head += (unsigned)n;
+#if OCX_GEN_INNER
+                if (total - produced >= (uint32_t)(RR * 64 + 64)) {
+                    // a whole batch still to draw: full rounds until the ring holds it, with
+                    // one loop test per round (no per-round need / last-round / batch tests;
+                    // every round here has 64 or more normals left to draw)
+                    do {
+                        const int n = zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane);
+                        produced += (uint32_t)n;
+                        head += (unsigned)n;
+                    } while (head < (unsigned)(RR * 64));
+                } else
+#endif
+                {
+                    const uint32_t left = total - produced;
+                    const int n =
+                        left >= 64u ? zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane)
+                                    : zig_round<true, false, true>(w, (int)left, tb, ring, 0, head,
+                                                                   lane);
+                    produced += (uint32_t)n;
+                    head += (unsigned)n;
+                }
                 if (head >= (unsigned)(RR * 64) || (produced == total && head > 0)) {
                     const int nrows = (int)(head >> 6) < RR ? (int)(head >> 6) : RR;
                     // lanes 8r..8r+7: row r's NumPy pairwise sum of squares, its clip scale
@@ -751,12 +769,23 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             const double* rp = ring + st1k.j0;
             const int64_t pstep = st1k.kstep * kst;
             while (produced < total) {
-                const uint32_t left = total - produced;
-                const int n = left >= 64u
-                                  ? zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane)
-                                  : zig_round<true>(w, (int)left, tb, ring, kFlat, head, lane);
-                produced += (uint32_t)n;
-                head += (unsigned)n;
+#if OCX_GEN_INNER
+                if (total - produced >= 1024u + 64u) {  // a whole row still to draw
+                    do {
+                        const int n = zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane);
+                        produced += (uint32_t)n;
+                        head += (unsigned)n;
+                    } while (head < 1024u);
+                } else
+#endif
+                {
+                    const uint32_t left = total - produced;
+                    const int n = left >= 64u
+                                      ? zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane)
+                                      : zig_round<true>(w, (int)left, tb, ring, kFlat, head, lane);
+                    produced += (uint32_t)n;
+                    head += (unsigned)n;
+                }
                 if (head >= 1024u) {
                     // NumPy's pairwise sum of squares: lanes 8l..8l+7 keep leaf l's eight
                     // accumulators (16 values each), the 64 partials combine in its order
