@@ -127,6 +127,18 @@ __device__ __noinline__ TailOut zig_tail(uint64_t st_lo, uint64_t st_hi, uint64_
     return o;
 }
 
+// Lane states (OCX_GEN_LANE_STATE): the round loop carries each lane's state for its next
+// draw instead of the uniform base.  After a round that consumed all 64 draws, state k + 64
+// = A^64·(state k) + C64 in every lane at once — the same 128-bit multiply-add as the jump
+// from the base, with a constant multiplier — so no readlanes of lane 63's state (nor the
+// wait for them) sit between one round and the next; a round that stops short rebuilds the
+// states from its last consumed draw (readlanes + the jump, as before).  The d = 64 rows
+// only (FLAT rounds): 62.4 -> 61.1 ms at 32 768 x 1e4, while the d = 1024 rows measured
+// 78.8 -> 80.5 ms (profiles/r03_gen_lanestate_ab.jsonl).
+#ifndef OCX_GEN_LANE_STATE
+#define OCX_GEN_LANE_STATE 1
+#endif
+
 // One stream, as a wave sees it: the uniform state and increment, and this lane's
 // jump-ahead pair (state after draw k of a round = Ak * base + Dk).  spec: this lane's
 // state of the NEXT round, formed ahead from lane 63's state (valid when `have_spec`, i.e.
@@ -137,6 +149,8 @@ struct WaveStream {
     ocx_u128 C64;  // inc·(A^63 + … + A + 1): the 64-draw jump's additive part (uniform)
     ocx_u128 spec;
     bool have_spec;
+    ocx_u128 s;     // OCX_GEN_LANE_STATE: this lane's state for the next round's draw
+    ocx_u128 C64v;  // C64 in every lane (a VGPR operand of the advance)
 };
 
 // Next round's base after a round that consumed all 64 draws: lane 63's state, which is
@@ -161,6 +175,13 @@ constexpr ocx_u128 pcg_gsum(int n) {  // A^(n-1) + … + A + 1
 }
 constexpr ocx_u128 kA64 = pcg_pow(64);
 constexpr ocx_u128 kG64 = pcg_gsum(64);
+constexpr ocx_u128 inv_u128(ocx_u128 a) {  // a^-1 mod 2^128 (a odd): Newton, 3 -> 384 bits
+    ocx_u128 x = a;
+    for (int i = 0; i < 7; ++i) x = x * (2 - a * x);
+    return x;
+}
+constexpr ocx_u128 kAinv = inv_u128(OCX_PCG_MULT);
+static_assert(kAinv * OCX_PCG_MULT == 1, "PCG multiplier inverse");
 
 // ---- (a * b + d) mod 2^128 with a, d per lane and b wave-uniform (SGPRs) --------------
 // Ten 32x32 partial products: six v_mad_u64_u32 (the 64-bit columns, each keeping its
@@ -223,6 +244,15 @@ __device__ __forceinline__ ocx_u128 mul_add_u128(ocx_u128 a, ocx_u128 b, ocx_u12
 #endif
 }
 
+// a copy the compiler cannot prove uniform: it stays in VGPRs (no per-round SGPR → VGPR moves)
+__device__ __forceinline__ ocx_u128 vcopy128(ocx_u128 v) {
+    uint32_t q[4] = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("v_mov_b32 %0, %1" : "=v"(q[i]) : "v"(q[i]));
+    return ((ocx_u128)q[3] << 96) | ((ocx_u128)q[2] << 64) | ((ocx_u128)q[1] << 32) | q[0];
+}
+
+template <bool LS>
 __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u128 Gk) {
     // every lane holds the same state; reading it from lane 0 makes it provably uniform,
     // so the round loop keeps the base in SGPRs (the multiply's scalar operand)
@@ -231,6 +261,18 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
     w.Dk = g.inc * Gk;
     w.C64 = rl128(g.inc, 0) * kG64;
     w.have_spec = false;
+    if constexpr (LS) {
+        w.C64v = vcopy128(w.C64);
+        w.s = mul_add_u128(w.Ak, w.base, w.Dk);
+    }
+}
+
+// The base of the stream (the state of the last draw consumed) from the lane states:
+// lane 0's state is A·base + inc.  Only where something reads the base (the labels, saved
+// states) — the round loop itself carries the lane states.
+template <bool LS>
+__device__ __forceinline__ void ws_sync_base(WaveStream& w) {
+    if constexpr (LS) w.base = rl128(kAinv * (rl128(w.s, 0) - rl128(w.inc, 0)), 0);
 }
 
 // One round: speculate 64 draws, parse them in stream order, append at most `need`
@@ -254,12 +296,17 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
 #ifndef OCX_GEN_INNER
 #define OCX_GEN_INNER 1
 #endif
+// labels through LDS, one 32-B segment per step and block (see the kernel)
+#ifndef OCX_GEN_STAGE_Y
+#define OCX_GEN_STAGE_Y 1
+#endif
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.
 template <bool RING, bool FULL = false, bool FLAT = false>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
     const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
+    constexpr bool LS = FLAT && OCX_GEN_LANE_STATE;  // lane states (d = 64 rows)
 #if OCX_GEN_SPEC_NEXT
     ocx_u128 s;
     if (w.have_spec) {  // wave-uniform
@@ -270,7 +317,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const ocx_u128 s63 = rl128(s, 63);
     w.spec = mul_add_u128(w.Ak, s63, w.Dk);
 #else
-    const ocx_u128 s = mul_add_u128(w.Ak, w.base, w.Dk);
+    const ocx_u128 s = LS ? w.s : mul_add_u128(w.Ak, w.base, w.Dk);
 #endif
     const uint64_t r = xsl_rr(s);
     const int idx = (int)(r & 0xff);
@@ -294,7 +341,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #elif OCX_GEN_SCALAR_NEXT
         w.base = w.base * kA64 + w.C64;
 #else
-        w.base = rl128(s, 63);
+        if constexpr (LS) w.s = mul_add_u128(s, kA64, w.C64v);
+        else w.base = rl128(s, 63);
 #endif
         return 64;
     }
@@ -325,7 +373,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
                 const bool skip = lane == k + 1 || (!wa && lane == k);
                 if (RING && !skip)
                     ring[(head + (unsigned)lane - (lane > k + 1 ? sh : 0u)) & fmask] = x;
-                w.base = rl128(s, 63);
+                w.base = rl128(s, 63);  // (not FLAT: no lane states)
                 return wa ? 63 : 62;
             }
         }
@@ -425,6 +473,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
                                    (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
         if (RING && lane == 0) ring[(head + n) & fmask] = o.v;
         w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
+        if constexpr (LS) w.s = mul_add_u128(w.Ak, w.base, w.Dk);
 #if OCX_GEN_SPEC_NEXT
         w.have_spec = false;
 #endif
@@ -443,6 +492,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #else
     w.base = rl128(s, m - 1);
 #endif
+    if constexpr (LS)
+        w.s = m == 64 ? mul_add_u128(s, kA64, w.C64v) : mul_add_u128(w.Ak, rl128(s, m - 1), w.Dk);
     return n;
 }
 
@@ -553,9 +604,22 @@ __device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, 
     has32 = (int)(p[4] >> 32);
 }
 
-constexpr int kWaveBlock = 256;
+// Waves per block of the default d = 64 form (OCX_GEN_NW64): a block's waves hold
+// consecutive sequences, so the staged labels (see the kernel) leave as NW·8-B segments per
+// step (up to a whole 128-B line of the y tile at S = 16).  32 768 x 1e4 at d = 64: 63.9 /
+// 62.6 / 65.5 ms with 4 / 8 / 16 waves per block (profiles/r03_gen_nw_ab.jsonl; 16 makes
+// every label round wait for the slowest of 16 waves).  The other forms keep 4 (their LDS
+// then still admits their occupancy).
+#ifndef OCX_GEN_NW64
+#define OCX_GEN_NW64 8
+#endif
+__host__ __device__ constexpr int gen_block(int DF, bool LR) {
+    return 64 * ((DF == 64 && !LR) ? OCX_GEN_NW64 : 4);
+}
 #ifdef OCX_GEN_TUNE_NO_STORE  // tuning only: rows computed, not written
 #define OCX_GEN_STORE(v, p) do { if ((v) == 1234.5) *(p) = (v); } while (0)
+#elif defined(OCX_GEN_PLAIN_STORE)  // tuning: write-back z stores
+#define OCX_GEN_STORE(v, p) (*(p) = (v))
 #else
 #define OCX_GEN_STORE(v, p) __builtin_nontemporal_store((v), (p))
 #endif
@@ -604,12 +668,16 @@ constexpr int kRows64 = 8;
 // RAW (DF = 0 only): rows left unclipped, for the float32 twin (ocx_twin32.hip), which
 // rounds them to float and clips them in float32 itself (algorithms.py:157-160).
 template <int MODE, int DF, bool LR = false, bool RAW = false>
-__global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
+__global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
     const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out, int rb,
     int64_t nwaves) {
+    constexpr int kBlock = gen_block(DF, LR);
+    constexpr int kNW = kBlock / 64;
+    // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
+    constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && DF == 64;
     __shared__ ZigTables tb;
     extern __shared__ double rings[];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -623,7 +691,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     // stream index b: the per-stream SeedSequence hashing then runs on the scalar unit
     // beside other waves' VALU work instead of on 64 identical lanes
     const int64_t wave = __builtin_amdgcn_readfirstlane(
-        (int)(blockIdx.x * (kWaveBlock / 64) + (threadIdx.x >> 6)));
+        (int)(blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)));
     if (wave >= nwaves) return;
     const int slot = rb + (DF == 0 && d_arg > 128 ? kStackDoubles : 0);  // ring (+ pairwise stack)
     double* ring = rings + (threadIdx.x >> 6) * slot;
@@ -667,6 +735,35 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
     const int rl = Dp <= 64 ? lane / Dp : 0;
     const int cl = jl / C, kl = (jl - cl * C) >> 1, el = (jl - cl * C) & 1;
 
+    // Labels through LDS (stage_y): the kNW waves of a block hold kNW consecutive sequences,
+    // so each step's labels of the block are min(kNW, S) contiguous, aligned doubles of the y
+    // tile.  Each wave leaves a round's 128 labels at the front of its own ring and the block
+    // stores them together, kNW lanes per step, instead of each wave's 8-B stores each costing
+    // a whole write granule (WRITE_SIZE 1.052x the algorithmic bytes at d = 64, ~35 B per
+    // 8-B label; profiles/r02_traffic_gen_final.json, r03_gen_ystage_*).  Every wave of a
+    // block runs the same number of sequences and label rounds (fresh streams only: the chunk
+    // mode's buffered half-draw makes rounds differ per sequence; nseq and nwaves multiples of
+    // kNW, checked here and arranged by the launcher).
+    const bool stage_y = OCX_GEN_STAGE_Y && MODE == 0 && lab_in == nullptr &&
+                         nwaves % kNW == 0 && nseq % kNW == 0;
+    // b0: the block's first sequence of this pass (the block's waves hold b0 .. b0 + kNW - 1)
+    auto store_y_round = [&](int64_t tl, int64_t b0) {
+        __syncthreads();  // every wave's round is in its ring
+        const int tid = (int)threadIdx.x;
+        const int64_t left = T - tl;
+        const int Sq = 64 / P;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // 128 steps x kNW waves over kBlock threads
+            const int q = i * kBlock + tid;
+            const int tt = q / kNW, wv = q % kNW;
+            const int64_t bw = b0 + wv;
+            const int64_t gw = bw / Sq;
+            if (tt < left)
+                __builtin_nontemporal_store(rings[wv * slot + tt],
+                                            ytl + (gw * T + tl + tt) * Sq + (bw - gw * Sq));
+        }
+        __syncthreads();  // the rings are free again
+    };
     for (int64_t b = wave; b < nseq; b += nwaves) {
         const int64_t g = b / S;
         const int s = (int)(b - g * S);
@@ -681,7 +778,16 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             for (int64_t t = 0; t < T; ++t)
                 for (int j = lane; j < Dp; j += 64) *zaddr(t, j) = 0.0;
             if (b >= B) {
-                for (int64_t t = lane; t < T; t += 64) yrow[t * S] = 0.0;
+                if (stage_y) {
+                    // the block's label rounds (and barriers) with zeros for this sequence
+                    for (int64_t tl = 0; tl < T; tl += 128) {
+                        ring[2 * lane] = 0.0;
+                        ring[2 * lane + 1] = 0.0;
+                        store_y_round(tl, b - (b % kNW));
+                    }
+                } else {
+                    for (int64_t t = lane; t < T; t += 64) yrow[t * S] = 0.0;
+                }
                 continue;
             }
         }
@@ -692,7 +798,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             ocx_rng_init3(&g0, base_seed, (uint64_t)T_seed, (uint64_t)(run0 + b));
             if (MODE == 1 && lane == 0) save_state6(st_out + 6 * b, g0.state, g0.inc, 0, 0);
         }
-        ws_set(w, g0, Gk);
+        ws_set<kLS>(w, g0, Gk);
 
         // ---- rows
         if constexpr (MODE == 0 && DF == 64) {
@@ -909,6 +1015,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             }
         }
         }  // generic row loop
+        ws_sync_base<kLS>(w);
         if (MODE == 1) {
             if (lane == 0) save_state6(lab_out + 6 * b, w.base, w.inc, 0, 0);
             continue;
@@ -925,7 +1032,7 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             w.base = rl128(ls, 0);
         }
         int64_t tl = 0;
-        if (has32 && T > 0) {
+        if (has32 && T > 0) {  // (chunk mode only: never with stage_y)
             if (lane == 0) yrow[0] = (buf32 >> 31) ? 1.0 : -1.0;
             has32 = 0;
             tl = 1;
@@ -936,7 +1043,11 @@ __global__ __launch_bounds__(kWaveBlock, OCX_GENW_MIN_WAVES_FOR(DF, LR)) void oc
             const ocx_u128 st = mul_add_u128(w.Ak, w.base, w.Dk);
             const uint64_t r = xsl_rr(st);
             const int64_t t0 = tl + 2 * lane;
-            if (lane < ndraw) {
+            if (stage_y) {
+                ring[2 * lane] = (((uint32_t)r) >> 31) ? 1.0 : -1.0;
+                ring[2 * lane + 1] = (((uint32_t)(r >> 32)) >> 31) ? 1.0 : -1.0;
+                store_y_round(tl, b - (b % kNW));
+            } else if (lane < ndraw) {
                 yrow[t0 * S] = (((uint32_t)r) >> 31) ? 1.0 : -1.0;
                 if (t0 + 1 < T) yrow[(t0 + 1) * S] = (((uint32_t)(r >> 32)) >> 31) ? 1.0 : -1.0;
             }
@@ -967,9 +1078,10 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
                           int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
                           double* ytl, const uint64_t* st_in, uint64_t* st_out,
                           const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
+    constexpr int kBlock = gen_block(DF, LR);
     const int rb = (MODE == 0) ? ring_doubles(d, DF, LR) : 0;
     const size_t lds =
-        (MODE == 0) ? (size_t)(rb + (DF == 0 && d > 128 ? kStackDoubles : 0)) * 8 * (kWaveBlock / 64) : 0;
+        (MODE == 0) ? (size_t)(rb + (DF == 0 && d > 128 ? kStackDoubles : 0)) * 8 * (kBlock / 64) : 0;
     // resident waves: fill the GPU once, sequences spread evenly over the waves
     int dev = 0, cus = 256, per_cu = 0;
     hipError_t e = hipGetDevice(&dev);
@@ -993,13 +1105,13 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
         if (it == cache.end()) {
             int q = 0;
             e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &q, ocx_gen_wave_kernel<MODE, DF, LR, RAW>, kWaveBlock, lds);
+                &q, ocx_gen_wave_kernel<MODE, DF, LR, RAW>, kBlock, lds);
             if (e != hipSuccess) return e;
             it = cache.emplace(key, q).first;
         }
         per_cu = it->second;
     }
-    int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kWaveBlock / 64);
+    int64_t waves_per_cu = (int64_t)std::max(per_cu, 1) * (kBlock / 64);
     // OCX_GEN_WAVES_PER_SIMD caps the resident generator waves (leaves registers free for
     // a kernel running beside it on another stream)
     if (const char* ev = std::getenv("OCX_GEN_WAVES_PER_SIMD")) {
@@ -1008,9 +1120,12 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     }
     const int64_t resident = std::max<int64_t>(1, (int64_t)cus * waves_per_cu);
     const int64_t per_wave = (nseq + resident - 1) / resident;
-    const int64_t nwaves = (nseq + per_wave - 1) / per_wave;
-    const unsigned blocks = (unsigned)((nwaves + (kWaveBlock / 64) - 1) / (kWaveBlock / 64));
-    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR, RAW>), dim3(blocks), dim3(kWaveBlock), lds, st,
+    const unsigned blocks =
+        (unsigned)(((nseq + per_wave - 1) / per_wave + (kBlock / 64) - 1) / (kBlock / 64));
+    // every block full (a multiple of 4 waves: the staged label stores, see the kernel); the
+    // waves past the last sequence run no sequence
+    const int64_t nwaves = (int64_t)blocks * (kBlock / 64);
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR, RAW>), dim3(blocks), dim3(kBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
                        st_out, lab_in, lab_out, rb, nwaves);
     return hipGetLastError();

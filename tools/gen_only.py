@@ -1,5 +1,5 @@
 """Launch only the g(T) generator on one resident batch (for rocprofv3 counter passes):
-    python tools/gen_only.py B T d [launches]"""
+    python tools/gen_only.py B T d [launches] [lanes_per_seq]"""
 import os
 import sys
 import time
@@ -13,7 +13,8 @@ def main():
     from online_convex_optimization_amd import engine
     B, T, d = (int(v) for v in sys.argv[1:4])
     n = int(sys.argv[4]) if len(sys.argv) > 4 else 1
-    db = engine.DeviceBatch(B, T, d)
+    kw = {"lanes_per_seq": int(sys.argv[5])} if len(sys.argv) > 5 else {}
+    db = engine.DeviceBatch(B, T, d, **kw)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n):

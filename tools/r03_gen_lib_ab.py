@@ -31,9 +31,11 @@ def main():
             assert L.ocx_dev_gen_gT(ctypes.byref(db.L), 0, 0, db.z.data_ptr(), db.y.data_ptr(),
                                     ctypes.c_void_p(st.cuda_stream)) == 0
             zs = db.z.view(torch.int64)
+            ys = db.y.view(torch.int64)
             sums.append((int(zs.sum().item()), int(zs[::7].sum().item()),
-                         int(db.y.view(torch.int64).sum().item())))
-        del zs  # a view of db.z: it would keep the batch alive into the next shape
+                         int(ys.sum().item()), int(ys[::7].sum().item()),
+                         int(ys[::13].sum().item())))
+        del zs, ys  # views of db.z: it would keep the batch alive into the next shape
         same = all(x == sums[0] for x in sums)
         print(json.dumps({"B": B, "T": T, "d": d, "bit_identical": bool(same)}), flush=True)
         if not same:
