@@ -76,6 +76,14 @@ def parse():
     return ap.parse_args()
 
 
+def alg_kernel_name(L) -> str:
+    """The FTRL kernel a DeviceBatch.simulate_alg launch runs for layout L (ocx_sim.hip
+    ocx_launch_alg): the pipelined butterfly kernel where ocx_pipe_supported holds."""
+    pipe = (not L.chain and L.P in (8, 16, 32) and L.C in (4, 8, 16, 32)
+            and not os.environ.get("OCX_ALG_NO_PIPE"))
+    return "ocx_alg_pipe_kernel" if pipe else "ocx_alg_kernel"
+
+
 def cpu_baseline(T, d, runs, budget_s):
     """Oracle (C restatement, 1 thread) on the first sequences of the same workload."""
     from oracle import oracle as O
@@ -367,7 +375,7 @@ def main():
                        "z_bytes_per_gpu": db.z_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                         "kernel": "ocx_alg_kernel", "kernel_ms": kern_ms,
+                         "kernel": alg_kernel_name(db.L), "kernel_ms": kern_ms,
                          "alg_bytes_per_launch": alg_bytes,
                          "bytes_per_timestep": alg_bytes / (B * T)},
             # SURVEY 8(d) prices a timestep at 2*(8d+8) = 1040 B (the reference reads z twice).

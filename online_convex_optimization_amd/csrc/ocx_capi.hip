@@ -182,11 +182,16 @@ int ocx_layout_init(int64_t B, int64_t T, int64_t d, int lanes_per_seq, ocx_layo
     // T = 1e5, 3328 sequences measured 69 ms at 16 x 4 (62 % of 8 TB/s) against 75 ms at
     // 8 x 8, 82 ms at 32 x 2 and 104 ms for the exact 8-lane chain; d = 1024: 52 ms
     // (81 %) against 102 ms exact (profiles/r02_fewwave_block_shapes.jsonl)
+    // Since round 3 the pipelined butterfly kernel (ocx_alg_pipe.hip) also wins on the big
+    // resident batches at 64 <= d <= 128 from 4096 sequences on: d = 64, 32 768 x 1e4, one
+    // pass over z: 26.6 ms at 8 x 8 against 27.05 ms for the exact 4 x 16 chain, and the
+    // generator writes whole 128-B lines of the 8 x 8 tile (59.5 vs 60.8 ms; WRITE_SIZE
+    // 1.00002x vs 1.024x; profiles/r03_e2e_layout.jsonl, r03_traffic_gen_p8.json).
     bool best_tree = false;  // OCX_LANES_BEST fell back to butterfly sums
     if (lanes_per_seq == OCX_LANES_BEST) {
         ocx_layout Le;
         if (int rc = ocx_layout_init(B, T, d, 1, &Le)) return rc;
-        if (Le.P < 8) {
+        if (Le.P < 8 && !(d >= 64 && d <= 128 && B >= 4096)) {
             *L = Le;
             return OCX_OK;
         }

@@ -82,12 +82,16 @@ def test_auto_layout_choices():
 
 
 def test_best_layout_choices():
-    """OCX_LANES_BEST (128): the exact layout while its chains stay under 8 lanes, else
-    butterfly sums with 8 coordinates per lane up to d = 128 (4 below 4096 sequences), 32
-    from d = 512."""
+    """OCX_LANES_BEST (128): the exact layout while its chains stay under 8 lanes, except
+    the big batches at 64 <= d <= 128 (>= 4096 sequences); else butterfly sums with 8
+    coordinates per lane up to d = 128 (4 below 4096 sequences), 32 from d = 512."""
     best = 128
-    L = _lib.layout(32768, 10, 64, best)       # the bench batch: exact, 4-lane chain
+    L = _lib.layout(32768, 10, 64, best)       # the bench batch: butterfly 8 x 8
+    assert (L.P, L.C, L.chain) == (8, 8, 0)
+    L = _lib.layout(32768, 10, 64, 1)          # its exact layout: a 4-lane chain
     assert (L.P, L.C, L.chain) == (4, 16, 1)
+    L = _lib.layout(32768, 10, 32, best)       # d < 64: exact
+    assert L.chain == 1 or L.P == 1
     L = _lib.layout(65536, 10, 16, best)       # configs[1]: exact, one lane per sequence
     assert (L.P, L.chain) == (1, 0)
     L = _lib.layout(768, 10, 5, best)          # the drivers' batches: exact
