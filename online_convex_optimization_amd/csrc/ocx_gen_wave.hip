@@ -39,11 +39,39 @@ constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 #define OCX_GEN_WEDGE_F32 0
 #endif
 
+// The fast path's table lookup (ki[idx], wi[idx] for a random layer idx per lane) as one
+// ds_read_b128 of an interleaved {ki, wi} entry (OCX_GEN_KW128): the two tables read as a
+// ds_read2_b64 bank on (a/4) mod 32 in 16-lane groups, so 16 random layers fall into 16
+// slots per access and pass twice; a b128 read banks on (a/4) mod 64 and passes once.
+// Bit-identical and time-neutral (32 768 x 1e4 x 64: 59.76 vs 59.76 ms; 2 048 x 1e4 x 1024:
+// 77.47 vs 77.52; profiles/r03_gen_kw_ab.jsonl): the LDS is not what bounds the generator.
+#ifndef OCX_GEN_KW128
+#define OCX_GEN_KW128 1
+#endif
+struct alignas(16) ZigKW {
+    uint64_t ki;
+    double wi;
+};
 struct ZigTables {
+#if OCX_GEN_KW128
+    ZigKW kw[256];
+#else
     uint64_t ki[256];
     double wi[256];
+#endif
     double fi[256];
 };
+__device__ __forceinline__ void zig_lookup(const ZigTables& tb, int idx, uint64_t& ki, double& wi) {
+#if OCX_GEN_KW128
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *reinterpret_cast<const u32x4*>(&tb.kw[idx]);
+    ki = ((uint64_t)v.y << 32) | v.x;
+    wi = __hiloint2double((int)v.w, (int)v.z);
+#else
+    ki = tb.ki[idx];
+    wi = tb.wi[idx];
+#endif
+}
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
@@ -296,13 +324,48 @@ __device__ __forceinline__ void ws_sync_base(WaveStream& w) {
 #ifndef OCX_GEN_INNER
 #define OCX_GEN_INNER 1
 #endif
+// The d = 64 inner do-while of full rounds, two rounds per trip: the lane states alternate
+// between two register sets instead of being copied at the back edge (32 768 x 1e4 x 64:
+// 59.9 -> 59.4 ms, 58.7 -> 58.1 on a second box; the d = 1024 rows, without lane states,
+// measured slower: 77.5 -> 78.8 ms; profiles/r03_gen_swz_ab.jsonl, r03_gen_variants4_ab.jsonl)
+#ifndef OCX_GEN_UNROLL
+#define OCX_GEN_UNROLL 2
+#endif
+// d = 1024 rows with the d = 64 form's round (FLAT: unmasked ring, lane states): measured
+// 80.4 vs 77.2 ms (profiles/r03_gen_variants4_ab.jsonl); off, a tuning knob
+#ifndef OCX_GEN_1K_FLAT
+#define OCX_GEN_1K_FLAT 0
+#endif
+// lane states: the next round's states formed before this round's table lookup, to overlap
+// the lookup's latency: 60.6 vs 58.1 ms at 32 768 x 1e4 x 64 (r03_gen_variants4_ab.jsonl:
+// four more live VGPRs, no latency to hide); off, a tuning knob
+#ifndef OCX_GEN_LS_EARLY
+#define OCX_GEN_LS_EARLY 0
+#endif
 // labels through LDS, one 32-B segment per step and block (see the kernel)
 #ifndef OCX_GEN_STAGE_Y
 #define OCX_GEN_STAGE_Y 1
 #endif
+// Swizzled ring of the d = 1024 rows (OCX_GEN_SWZ1K).  The row's epilogue reads the ring
+// with strides that put a whole 32-lane half on one LDS bank pair: the 32 x 32 store map
+// reads slot 32·(l/2) + (l%2) + 2i (16-way) and the pairwise sum slot 128·(l/8) + l%8 + 8q
+// (4-way; ds_read_b64 banks repeat every 32 doubles).  Slot i lives at i ^ (bits 5..8 of i
+// moved to bits 1..4): a permutation inside each aligned 32-double block, so the round's
+// contiguous writes stay conflict-free and both epilogue reads hit 32 distinct bank pairs.
+// Bit-identical; 2 048 x 1e4 x 1024: 79.2 -> 77.5 ms, SQ_LDS_BANK_CONFLICT 1.82e10 -> 7.55e9
+// cycles (profiles/r03_gen_swz_ab.jsonl, r03_pmc_gen1k_lds.json).
+#ifndef OCX_GEN_SWZ1K
+#define OCX_GEN_SWZ1K 1
+#endif
+template <int SW>
+__device__ __forceinline__ unsigned rix(unsigned i) {
+    if constexpr (SW == 1) return i ^ ((i >> 4) & 30u);
+    else return i;
+}
+
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
-// left to the front itself): ring indices go unmasked.
-template <bool RING, bool FULL = false, bool FLAT = false>
+// left to the front itself): ring indices go unmasked.  SW: the ring's slot map (rix).
+template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
                          unsigned head, int lane) {
     const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
@@ -319,29 +382,39 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
 #else
     const ocx_u128 s = LS ? w.s : mul_add_u128(w.Ak, w.base, w.Dk);
 #endif
+#if OCX_GEN_LS_EARLY
+    const ocx_u128 s64 = LS ? mul_add_u128(s, kA64, w.C64v) : s;  // next round's, if m == 64
+#endif
     const uint64_t r = xsl_rr(s);
     const int idx = (int)(r & 0xff);
     const uint64_t r8 = r >> 8;
     const uint64_t rabs = (r8 >> 1) & kMask52;
-    double x = u52_to_double(rabs) * tb.wi[idx];
+    uint64_t kidx;
+    double widx;
+    zig_lookup(tb, idx, kidx, widx);
+    double x = u52_to_double(rabs) * widx;
     // sign bit 8 of the draw → the sign of x (x = -x, -0.0 included), one xor
     x = __hiloint2double(__double2hiint(x) ^ (int)(((uint32_t)r & 0x100u) << 23),
                          __double2loint(x));
 #ifdef OCX_GEN_TUNE_NO_PARSE  // tuning only: every draw accepted (wrong normals)
     const bool fast = true;
 #else
-    const bool fast = rabs < tb.ki[idx];
+    const bool fast = rabs < kidx;
 #endif
     const uint64_t rej = ballot(!fast);
     if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
-        if (RING) ring[(head + (unsigned)lane) & fmask] = x;
+        if (RING) ring[rix<SW>((head + (unsigned)lane) & fmask)] = x;
 #if OCX_GEN_SPEC_NEXT
         w.base = s63;
         w.have_spec = true;
 #elif OCX_GEN_SCALAR_NEXT
         w.base = w.base * kA64 + w.C64;
 #else
+#if OCX_GEN_LS_EARLY
+        if constexpr (LS) w.s = s64;
+#else
         if constexpr (LS) w.s = mul_add_u128(s, kA64, w.C64v);
+#endif
         else w.base = rl128(s, 63);
 #endif
         return 64;
@@ -372,7 +445,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
                 const unsigned sh = wa ? 1u : 2u;
                 const bool skip = lane == k + 1 || (!wa && lane == k);
                 if (RING && !skip)
-                    ring[(head + (unsigned)lane - (lane > k + 1 ? sh : 0u)) & fmask] = x;
+                    ring[rix<SW>((head + (unsigned)lane - (lane > k + 1 ? sh : 0u)) & fmask)] = x;
                 w.base = rl128(s, 63);  // (not FLAT: no lane states)
                 return wa ? 63 : 62;
             }
@@ -465,13 +538,13 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         n = need;
         tail_k = -1;
     }
-    if (RING && ((emit >> lane) & 1)) ring[(head + mbcnt(emit)) & fmask] = x;
+    if (RING && ((emit >> lane) & 1)) ring[rix<SW>((head + mbcnt(emit)) & fmask)] = x;
     if (tail_k >= 0) {
         // NumPy's tail loop, sequential from the state after the tail draw
         const ocx_u128 st = rl128(s, tail_k);
         const TailOut o = zig_tail((uint64_t)st, (uint64_t)(st >> 64), (uint64_t)w.inc,
                                    (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
-        if (RING && lane == 0) ring[(head + n) & fmask] = o.v;
+        if (RING && lane == 0) ring[rix<SW>((head + n) & fmask)] = o.v;
         w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
         if constexpr (LS) w.s = mul_add_u128(w.Ak, w.base, w.Dk);
 #if OCX_GEN_SPEC_NEXT
@@ -493,7 +566,11 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     w.base = rl128(s, m - 1);
 #endif
     if constexpr (LS)
+#if OCX_GEN_LS_EARLY
+        w.s = m == 64 ? s64 : mul_add_u128(w.Ak, rl128(s, m - 1), w.Dk);
+#else
         w.s = m == 64 ? mul_add_u128(s, kA64, w.C64v) : mul_add_u128(w.Ak, rl128(s, m - 1), w.Dk);
+#endif
     return n;
 }
 
@@ -677,12 +754,17 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
     constexpr int kBlock = gen_block(DF, LR);
     constexpr int kNW = kBlock / 64;
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
-    constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && DF == 64;
+    constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && (DF == 64 || (DF == 1024 && OCX_GEN_1K_FLAT));
     __shared__ ZigTables tb;
     extern __shared__ double rings[];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+#if OCX_GEN_KW128
+        tb.kw[i].ki = OCX_ZIG_KI[i];
+        tb.kw[i].wi = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
+#else
         tb.ki[i] = OCX_ZIG_KI[i];
         tb.wi[i] = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
+#endif
         tb.fi[i] = __longlong_as_double((long long)OCX_ZIG_FI_BITS[i]);
     }
     __syncthreads();
@@ -825,6 +907,14 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
                         const int n = zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane);
                         produced += (uint32_t)n;
                         head += (unsigned)n;
+#if OCX_GEN_UNROLL == 2
+                        // two rounds per trip: the state alternates between two register sets
+                        // (no back-edge copies of the 128-bit lane states)
+                        if (head >= (unsigned)(RR * 64)) break;
+                        const int n2 = zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane);
+                        produced += (uint32_t)n2;
+                        head += (unsigned)n2;
+#endif
                     } while (head < (unsigned)(RR * 64));
                 } else
 #endif
@@ -867,6 +957,8 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
             // (The ring is 1088 doubles: 4 waves' rings and the tables fill 160 KiB of LDS
             // with four 256-thread blocks, so the occupancy of the 1024 ring is kept.)
             constexpr int kFlat = 2047;  // every ring index is < 1088: masking is a no-op
+            constexpr int kSW = OCX_GEN_SWZ1K ? 1 : 0;
+            constexpr bool kF1k = OCX_GEN_1K_FLAT;
             const uint32_t total = (uint32_t)(T * 1024);
             uint32_t produced = 0;
             unsigned head = 0;
@@ -878,7 +970,7 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
 #if OCX_GEN_INNER
                 if (total - produced >= 1024u + 64u) {  // a whole row still to draw
                     do {
-                        const int n = zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane);
+                        const int n = zig_round<true, true, kF1k, kSW>(w, 64, tb, ring, kFlat, head, lane);
                         produced += (uint32_t)n;
                         head += (unsigned)n;
                     } while (head < 1024u);
@@ -887,43 +979,60 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
                 {
                     const uint32_t left = total - produced;
                     const int n = left >= 64u
-                                      ? zig_round<true, true>(w, 64, tb, ring, kFlat, head, lane)
-                                      : zig_round<true>(w, (int)left, tb, ring, kFlat, head, lane);
+                                      ? zig_round<true, true, kF1k, kSW>(w, 64, tb, ring, kFlat, head, lane)
+                                      : zig_round<true, false, kF1k, kSW>(w, (int)left, tb, ring,
+                                                                         kFlat, head, lane);
                     produced += (uint32_t)n;
                     head += (unsigned)n;
                 }
                 if (head >= 1024u) {
                     // NumPy's pairwise sum of squares: lanes 8l..8l+7 keep leaf l's eight
                     // accumulators (16 values each), the 64 partials combine in its order
+                    // slot 128a + b + 8q (a = lane/8, b = lane%8): its fields are disjoint, so
+                    // rix of it is (128a + b + 8(a%4)) ^ (8q + 2((q/4)%4)), a lane base xor a
+                    // constant
                     const unsigned o = (unsigned)((lane >> 3) * 128 + (lane & 7));
+                    const unsigned osw = kSW ? (o | (unsigned)(((lane >> 3) & 3) << 3)) : o;
                     double v[16];
 #pragma unroll
-                    for (int q = 0; q < 16; ++q) v[q] = ring[o + 8u * q];
+                    for (int q = 0; q < 16; ++q)
+                        v[q] = ring[kSW ? (osw ^ (8u * q + 2u * ((q >> 2) & 3))) : o + 8u * q];
                     double acc = v[0] * v[0];
 #pragma unroll
                     for (int q = 1; q < 16; ++q) acc += v[q] * v[q];
                     const double nrm = sqrt(ocx_seq_sum<64>(acc));
                     const double scr = 1.0 / (nrm > 1.0 ? nrm : 1.0);
                     double* zrow = zt + (int64_t)g * T * 128 + t * 128 + (int64_t)s * 2 * P;
-                    if (P <= 32) {
+                    if (kSW && P == 32) {
+                        // the 32 x 32 layout: slot 32·(l/2) + l%2 + 2i, rix = base ^ 2i with
+                        // base = 32·(l/2) + l%2 + 2·((l/2) % 16)
+                        double* zp = zrow + st1k.w0;
+                        const unsigned jb = (unsigned)st1k.j0 | (unsigned)(((lane >> 1) & 15) << 1);
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            __builtin_nontemporal_store(ring[jb ^ (2u * i)] * scr, zp + i * kst);
+                    } else if (P <= 32) {
                         double* zp = zrow + st1k.k0 * kst + st1k.w0;
 #pragma unroll
                         for (int i = 0; i < 16; ++i)
-                            __builtin_nontemporal_store(rp[i * st1k.jstep] * scr, zp + i * pstep);
+                            __builtin_nontemporal_store(
+                                ring[rix<kSW>((unsigned)(st1k.j0 + i * st1k.jstep))] * scr,
+                                zp + i * pstep);
                     } else {
 #pragma unroll 4
                         for (int i = 0; i < 16; ++i) {
                             const int f = i * 64 + lane;
                             const int k = f >> lg2P, wo = f & (2 * P - 1);
                             const int j = (wo >> 1) * C + 2 * k + (wo & 1);
-                            __builtin_nontemporal_store(ring[j] * scr, zrow + k * kst + wo);
+                            __builtin_nontemporal_store(ring[rix<kSW>((unsigned)j)] * scr,
+                                                        zrow + k * kst + wo);
                         }
                     }
                     // the spill moves to the front (LDS operations of a wave run in order:
                     // the row's reads above complete before these writes)
                     const unsigned ov = head - 1024u;
-                    const double sp = ring[1024 + (lane < 63 ? lane : 63)];
-                    if ((unsigned)lane < ov) ring[lane] = sp;
+                    const double sp = ring[rix<kSW>(1024u + (lane < 63 ? lane : 63))];
+                    if ((unsigned)lane < ov) ring[rix<kSW>((unsigned)lane)] = sp;
                     head = ov;
                     ++t;
                 }
