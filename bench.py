@@ -304,7 +304,8 @@ def main():
                 tr = json.load(f)
             want = "closed" if closed else "two-pass"
             if ((tr.get("B"), tr.get("T"), tr.get("d"), tr.get("P")) == (B, T, d, db.L.P)
-                    and tr.get("comparator", "two-pass") == want):
+                    and tr.get("comparator", "two-pass") == want
+                    and tr.get("kernel") == alg_kernel_name(db.L)):
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass

@@ -4,13 +4,17 @@
 // where the goldens were made; pinned against them, oracle.comparator_loss_blas_order):
 // * rows in groups of four (the 4x4 kernel): a 4-lane fma accumulation over the first
 //   m1 = d & ~3 coordinates, the lanes folded as (l0 + l2) + (l1 + l3);
-// * the T mod 4 last rows (the 4x1 kernel): 4-lane products added block after block;
+// * where T mod 4 >= 2, the next two rows (the 4x2 kernel): a 2-lane accumulation of plain
+//   products (lane j: coordinates 2i + j), l0 + l1;
+// * a last single row (the 4x1 kernel): 4-lane products added block after block;
 // * then the d mod 4 tail: 1 → fma(a0, x0, s); 2 → s + fma(a0, x0, a1 x1);
 //   3 → s + fma(a2, x2, fma(a0, x0, a1 x1));
-// * a one-row matrix (ddot): an fma chain for d < 16; 4 products per lane, folded
-//   ((a0 + a1) + a2) + a3 then (l0 + l2) + (l1 + l3), and an fma tail for 16 <= d < 32.
-// Rows of OpenBLAS's 4x2 kernel (T mod 4 >= 2, d >= 8) and one-row matrices with d >= 32
-// take the nearest of these orders (about one ulp per row).
+// * a one-row matrix (ddot): an fma chain for d < 16; from d = 16 four 8-lane fma
+//   accumulators over the first d & ~31 coordinates, each folded to 4 lanes (l_k + l_k+4),
+//   continued as four 4-lane fma accumulators over 16-coordinate blocks, then
+//   ((a0 + a1) + a2) + a3, (l0 + l2) + (l1 + l3) and an fma tail over d mod 16.
+// (The 4x2 rows and the d >= 32 ddot were probed in round 3; every row order is checked
+// against numpy by tests/test_oracle_golden.py::test_comparator_blas_order_matches_numpy.)
 // Two launches: one thread per row (|q_t - y_t| into a scratch row), then one thread per
 // sequence for the pairwise sum (leaves of <= 128 with 8 accumulators, halves cut at
 // multiples of 8, per 8192-element buffer).  Used by the exact_ftl drop-in, whose
@@ -32,19 +36,43 @@ __device__ double cb_row(const double* __restrict__ r, const double* __restrict_
             for (int64_t i = 0; i < d; ++i) s = fma(r[i], x[i], s);
             return s;
         }
-        double tot[4];
+        const int64_t n1 = d & ~(int64_t)15, n32 = d & ~(int64_t)31;
+        double acc[4][4], tot[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            tot[k] = ((r[k] * x[k] + r[4 + k] * x[4 + k]) + r[8 + k] * x[8 + k]) + r[12 + k] * x[12 + k];
+        for (int j = 0; j < 4; ++j) {
+            double a8[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a8[k] = 0.0;
+            for (int64_t b = 0; b < n32; b += 32) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) a8[k] = fma(r[b + 8 * j + k], x[b + 8 * j + k], a8[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[j][k] = a8[k] + a8[k + 4];
+            for (int64_t b = n32; b < n1; b += 16) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[j][k] = fma(r[b + 4 * j + k], x[b + 4 * j + k], acc[j][k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tot[k] = ((acc[0][k] + acc[1][k]) + acc[2][k]) + acc[3][k];
         s = cb_fold(tot);
-        for (int64_t i = 16; i < d; ++i) s = fma(r[i], x[i], s);
+        for (int64_t i = n1; i < d; ++i) s = fma(r[i], x[i], s);
         return s;
     }
     const int64_t m1 = d & ~(int64_t)3;
     double s = 0.0;
-    if (m1) {
+    const int64_t q4 = 4 * (T / 4);
+    if (m1 && T % 4 >= 2 && t >= q4 && t < q4 + 2) {  // 4x2 kernel
+        double a0 = r[0] * x[0], a1 = r[1] * x[1];
+        for (int64_t i = 2; i < m1; i += 2) {
+            a0 = a0 + r[i] * x[i];
+            a1 = a1 + r[i + 1] * x[i + 1];
+        }
+        s = a0 + a1;
+    } else if (m1) {
         double acc[4];
-        if (t < 4 * (T / 4)) {
+        if (t < q4) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[k] = 0.0;
             for (int64_t i = 0; i < m1; i += 4) {

@@ -555,12 +555,19 @@ def t32_empirical_worst_case_thresholds(T_grid, *, runs: int = 5, base_seed: int
 # and pinned against tests/golden (made by the reference itself):
 #   rows in groups of four (the 4x4 kernel): per row a 4-lane fma accumulation over the
 #     first m1 = d & ~3 coordinates, lanes summed as (l0 + l2) + (l1 + l3);
-#   the T mod 4 last rows (the 4x1 kernel): 4-lane products summed block after block with
-#     plain adds, the same lane fold;
+#   where T mod 4 >= 2, the next two rows (the 4x2 kernel): per row a 2-lane accumulation
+#     of plain products over the first m1 coordinates (lane j: coordinates 2i + j), l0 + l1;
+#   a last single row (T mod 4 = 1 or 3; the 4x1 kernel): 4-lane products summed block
+#     after block with plain adds, lanes (l0 + l2) + (l1 + l3);
 #   then the d mod 4 tail: 1 -> fma(a0, x0, s); 2 -> s + fma(a0, x0, a1 x1);
 #     3 -> s + fma(a2, x2, fma(a0, x0, a1 x1));
-#   a one-row matrix goes to ddot: an fma chain for d < 16, four 4-lane products folded
-#     ((a0 + a1) + a2) + a3, then (l0 + l2) + (l1 + l3) and an fma tail for 16 <= d < 32.
+#   a one-row matrix goes to ddot: an fma chain for d < 16; from d = 16 four 4-lane fma
+#     accumulators over 16-coordinate blocks — for the first d & ~31 coordinates four 8-lane
+#     fma accumulators over 32-coordinate blocks, each folded to 4 lanes as l_k + l_(k+4)
+#     before the 16-blocks continue them —, then ((a0 + a1) + a2) + a3,
+#     (l0 + l2) + (l1 + l3), and an fma tail over the last d mod 16 coordinates.
+#   (The 4x2 rows and the d >= 32 ddot were probed against numpy on this image in round 3:
+#   tests/test_oracle_golden.py::test_comparator_blas_order_matches_numpy.)
 # np.abs(r).sum(): NumPy's pairwise sum (float64, 8192-element buffers); then 0.5 * sum.
 from fractions import Fraction as _Fr  # noqa: E402
 
@@ -591,24 +598,39 @@ def dgemv_row(r, x, t: int, T: int) -> float:
             for i in range(d):
                 s = _fma64(r[i], x[i], s)
             return s
-        acc = [[r[4 * a + k] * x[4 * a + k] for k in range(4)] for a in range(4)]
+        n1, n32 = d & ~15, d & ~31
+        a8 = [[0.0] * 8 for _ in range(4)]
+        for b in range(0, n32, 32):
+            a8 = [[_fma64(r[b + 8 * j + k], x[b + 8 * j + k], a8[j][k]) for k in range(8)]
+                  for j in range(4)]
+        acc = [[a8[j][k] + a8[j][k + 4] for k in range(4)] for j in range(4)]
+        for b in range(n32, n1, 16):
+            acc = [[_fma64(r[b + 4 * j + k], x[b + 4 * j + k], acc[j][k]) for k in range(4)]
+                   for j in range(4)]
         tot = [((acc[0][k] + acc[1][k]) + acc[2][k]) + acc[3][k] for k in range(4)]
         s = (tot[0] + tot[2]) + (tot[1] + tot[3])
-        for i in range(16, d):
+        for i in range(n1, d):
             s = _fma64(r[i], x[i], s)
         return s
     m1 = d & ~3
     s = 0.0
     if m1:
-        if t < 4 * (T // 4):
+        q4 = 4 * (T // 4)
+        if t < q4:  # 4x4 kernel
             acc = [0.0] * 4
             for i in range(0, m1, 4):
                 acc = [_fma64(r[i + k], x[i + k], acc[k]) for k in range(4)]
-        else:
+            s = (acc[0] + acc[2]) + (acc[1] + acc[3])
+        elif T % 4 >= 2 and t < q4 + 2:  # 4x2 kernel
+            a2 = [r[0] * x[0], r[1] * x[1]]
+            for i in range(2, m1, 2):
+                a2 = [a2[j] + r[i + j] * x[i + j] for j in range(2)]
+            s = a2[0] + a2[1]
+        else:  # 4x1 kernel
             acc = [r[k] * x[k] for k in range(4)]
             for i in range(4, m1, 4):
                 acc = [acc[k] + r[i + k] * x[i + k] for k in range(4)]
-        s = (acc[0] + acc[2]) + (acc[1] + acc[3])
+            s = (acc[0] + acc[2]) + (acc[1] + acc[3])
     return _dgemv_tail(s, r[m1:], x[m1:])
 
 

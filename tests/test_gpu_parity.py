@@ -728,7 +728,8 @@ def test_streamed_closed_form_fallback(ocx, monkeypatch, P):
 
 
 @pytest.mark.parametrize("T,d", [(1, 3), (1, 20), (2, 8), (3, 5), (7, 13), (130, 5), (9000, 5),
-                                 (65, 64), (12, 1024)])
+                                 (65, 64), (12, 1024), (1, 32), (1, 77), (1, 1024), (2, 37),
+                                 (6, 64), (7, 9), (11, 130), (130, 64)])
 def test_comparator_loss_blas_order(ocx, T, d):
     """ocx_comparator_loss_blas_batch == the oracle's dgemv_t / pairwise order bit for bit
     (pinned on the goldens in test_oracle_golden), and == NumPy on this host to 1e-15."""

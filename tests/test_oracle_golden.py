@@ -57,6 +57,38 @@ def test_exact_ftl_run_ftrl_and_replay(golden):
         assert O.replay_cum_loss(z, y, acts) == F(rec["replay"]["cum_loss"]), name
 
 
+def _openblas_arch():
+    try:
+        import threadpoolctl
+        for i in threadpoolctl.threadpool_info():
+            if i.get("internal_api") == "openblas":
+                return i.get("architecture"), i.get("version")
+    except Exception:  # pragma: no cover - threadpoolctl absent
+        pass
+    return None, None
+
+
+@pytest.mark.skipif(_openblas_arch() != ("SkylakeX", "0.3.29"),
+                    reason="the dgemv/ddot orders were probed on OpenBLAS 0.3.29's SkylakeX "
+                           "kernels (this image, where the goldens were made)")
+def test_comparator_blas_order_matches_numpy():
+    """exact_ftl.py:224-227 `0.5 * np.abs(z @ x - y).sum()` in the oracle's explicit order
+    equals NumPy on this image bit for bit, on every row kernel OpenBLAS's dgemv_t picks
+    (4x4 groups, the 4x2 pair where T mod 4 >= 2, the 4x1 last row, one-row ddot with its
+    8-lane blocks from d = 32) and every d mod 4 / d mod 16 / d mod 32 tail."""
+    rng = np.random.default_rng(11)
+    n = 0
+    for T in (1, 2, 3, 5, 6, 7, 10, 11):
+        for d in list(range(1, 41)) + [47, 63, 64, 65, 96, 127, 129, 200, 1024]:
+            z = rng.standard_normal((T, d))
+            y = np.where(rng.random(T) < 0.5, -1.0, 1.0)
+            x = rng.standard_normal(d)
+            want = 0.5 * float(np.abs(z @ x - y).sum())
+            assert O.comparator_loss_blas_order(z, y, x) == want, (T, d)
+            n += 1
+    assert n == 8 * 49
+
+
 def test_seeded_gT_sequences(golden):
     for rec in golden.j["seeded_gT"]:
         z, y = O.gT_sample(rec["base_seed"], rec["T"], rec["run"], rec["d"])
