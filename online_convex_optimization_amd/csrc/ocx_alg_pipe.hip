@@ -43,6 +43,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
     // is an SGPR base + the lane's constant offset, with no per-load address arithmetic
     const int64_t g = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_wave_id());
     if (g >= G) return;
+#ifdef OCX_ALG_PRIO  // tuning: issue priority over waves of a kernel running beside it
+    __builtin_amdgcn_s_setprio(OCX_ALG_PRIO);
+#endif
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;

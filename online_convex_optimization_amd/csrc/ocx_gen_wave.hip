@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 
 #include "ocx_internal.h"
@@ -39,38 +40,45 @@ constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 #define OCX_GEN_WEDGE_F32 0
 #endif
 
-// The fast path's table lookup (ki[idx], wi[idx] for a random layer idx per lane) as one
-// ds_read_b128 of an interleaved {ki, wi} entry (OCX_GEN_KW128): the two tables read as a
-// ds_read2_b64 bank on (a/4) mod 32 in 16-lane groups, so 16 random layers fall into 16
-// slots per access and pass twice; a b128 read banks on (a/4) mod 64 and passes once.
-// Bit-identical and time-neutral (32 768 x 1e4 x 64: 59.76 vs 59.76 ms; 2 048 x 1e4 x 1024:
-// 77.47 vs 77.52; profiles/r03_gen_kw_ab.jsonl): the LDS is not what bounds the generator.
-#ifndef OCX_GEN_KW128
-#define OCX_GEN_KW128 1
+// The fast path's table lookup (ki[idx], wi[idx] for a random layer idx per lane) is one
+// ds_read_b128 of an interleaved {ki, wi} entry: the two separate tables read as a
+// ds_read2_b64, which banks on (a/4) mod 32 in 16-lane groups, so 16 random layers fall
+// into 16 slots per access and pass twice; a b128 read banks on (a/4) mod 64 and passes
+// once.  Bit-identical and time-neutral (32 768 x 1e4 x 64: 59.76 vs 59.76 ms; 2 048 x 1e4
+// x 1024: 77.47 vs 77.52; profiles/r03_gen_kw_ab.jsonl): the LDS is not what bounds the
+// generator.
+// KD: ki stored as a double.  ki < 2^53 and rabs < 2^52 are both exact doubles, so rabs < ki
+// is decided on the double the draw is converted to anyway and the integer rabs need not
+// stay live beside it (the tail path re-derives it from r): one VALU less per round.  Kept
+// for the d = 64 rows (32 768 x 1e4: 58.6 / 58.5 vs 58.9 / 58.9 ms); the d = 1024 kernel,
+// already at 128 VGPRs, spills more with it (76.7 / 76.8 vs 75.0 / 75.2 ms;
+// profiles/r03_gen_kid_ab.jsonl).
+#ifndef OCX_GEN_KI_DOUBLE
+#define OCX_GEN_KI_DOUBLE 1
 #endif
-struct alignas(16) ZigKW {
-    uint64_t ki;
-    double wi;
-};
+template <bool KD>
 struct ZigTables {
-#if OCX_GEN_KW128
-    ZigKW kw[256];
-#else
-    uint64_t ki[256];
-    double wi[256];
-#endif
+    struct alignas(16) Entry {
+        typename std::conditional<KD, double, uint64_t>::type ki;
+        double wi;
+    } kw[256];
     double fi[256];
 };
-__device__ __forceinline__ void zig_lookup(const ZigTables& tb, int idx, uint64_t& ki, double& wi) {
-#if OCX_GEN_KW128
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = *reinterpret_cast<const u32x4*>(&tb.kw[idx]);
-    ki = ((uint64_t)v.y << 32) | v.x;
-    wi = __hiloint2double((int)v.w, (int)v.z);
-#else
-    ki = tb.ki[idx];
-    wi = tb.wi[idx];
-#endif
+template <bool KD>
+__device__ __forceinline__ void zig_lookup(const ZigTables<KD>& tb, int idx,
+                                           typename std::conditional<KD, double, uint64_t>::type& ki,
+                                           double& wi) {
+    if constexpr (KD) {
+        typedef double f64x2 __attribute__((ext_vector_type(2)));
+        const f64x2 v = *reinterpret_cast<const f64x2*>(&tb.kw[idx]);
+        ki = v.x;
+        wi = v.y;
+    } else {
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 v = *reinterpret_cast<const u32x4*>(&tb.kw[idx]);
+        ki = ((uint64_t)v.y << 32) | v.x;
+        wi = __hiloint2double((int)v.w, (int)v.z);
+    }
 }
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int lane) {
@@ -365,8 +373,8 @@ __device__ __forceinline__ unsigned rix(unsigned i) {
 
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.  SW: the ring's slot map (rix).
-template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0>
-__device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* ring, int rmask,
+template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0, bool KD = false>
+__device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, double* ring, int rmask,
                          unsigned head, int lane) {
     const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
     constexpr bool LS = FLAT && OCX_GEN_LANE_STATE;  // lane states (d = 64 rows)
@@ -389,17 +397,20 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
     const int idx = (int)(r & 0xff);
     const uint64_t r8 = r >> 8;
     const uint64_t rabs = (r8 >> 1) & kMask52;
-    uint64_t kidx;
+    typename std::conditional<KD, double, uint64_t>::type kidx;
     double widx;
     zig_lookup(tb, idx, kidx, widx);
-    double x = u52_to_double(rabs) * widx;
+    const double xa = u52_to_double(rabs);  // (double)rabs, exactly
+    double x = xa * widx;
     // sign bit 8 of the draw → the sign of x (x = -x, -0.0 included), one xor
     x = __hiloint2double(__double2hiint(x) ^ (int)(((uint32_t)r & 0x100u) << 23),
                          __double2loint(x));
 #ifdef OCX_GEN_TUNE_NO_PARSE  // tuning only: every draw accepted (wrong normals)
     const bool fast = true;
 #else
-    const bool fast = rabs < kidx;
+    bool fast;
+    if constexpr (KD) fast = xa < kidx;
+    else fast = rabs < kidx;
 #endif
     const uint64_t rej = ballot(!fast);
     if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
@@ -543,7 +554,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables& tb, double* r
         // NumPy's tail loop, sequential from the state after the tail draw
         const ocx_u128 st = rl128(s, tail_k);
         const TailOut o = zig_tail((uint64_t)st, (uint64_t)(st >> 64), (uint64_t)w.inc,
-                                   (uint64_t)(w.inc >> 64), rl64(rabs, tail_k));
+                                   (uint64_t)(w.inc >> 64),
+                                   KD ? (rl64(r, tail_k) >> 9) & kMask52 : rl64(rabs, tail_k));
         if (RING && lane == 0) ring[rix<SW>((head + n) & fmask)] = o.v;
         w.base = rl128(((ocx_u128)o.hi << 64) | o.lo, 0);  // uniform (see ws_set)
         if constexpr (LS) w.s = mul_add_u128(w.Ak, w.base, w.Dk);
@@ -755,16 +767,12 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
     constexpr int kNW = kBlock / 64;
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
     constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && (DF == 64 || (DF == 1024 && OCX_GEN_1K_FLAT));
-    __shared__ ZigTables tb;
+    constexpr bool kKD = OCX_GEN_KI_DOUBLE && DF == 64;  // ki as doubles (see ZigTables)
+    __shared__ ZigTables<kKD> tb;
     extern __shared__ double rings[];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-#if OCX_GEN_KW128
-        tb.kw[i].ki = OCX_ZIG_KI[i];
+        tb.kw[i].ki = (decltype(tb.kw[i].ki))OCX_ZIG_KI[i];  // < 2^53: exact as a double
         tb.kw[i].wi = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
-#else
-        tb.ki[i] = OCX_ZIG_KI[i];
-        tb.wi[i] = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
-#endif
         tb.fi[i] = __longlong_as_double((long long)OCX_ZIG_FI_BITS[i]);
     }
     __syncthreads();
