@@ -30,10 +30,12 @@
  *              lane (layout.chain = 1);
  *       OCX_LANES_BEST (128)  the fastest certified mode, the default of the batched
  *              APIs: the exact layout's sums (value 1) wherever its lane chains are short
- *              (fewer than 8 lanes per sequence), where the kernels stream at the HBM
- *              roofline; butterfly sums otherwise (d >= 512, or few-wave batches such as
- *              the capacity-limited T = 1e5 g(T) batch), where a chain of 8+ lanes leaves
- *              the kernel latency-bound.  The g(T) and FTRL-vs-exact entry points also
+ *              (fewer than 8 lanes per sequence) and d < 64; butterfly sums otherwise —
+ *              d >= 512 and few-wave batches such as the capacity-limited T = 1e5 g(T)
+ *              batch, where a chain of 8+ lanes leaves the kernel latency-bound, and
+ *              batches of >= 4096 sequences at 64 <= d <= 128, where the pipelined 8 x 8
+ *              butterfly kernel beats the 4-lane chain and the generator writes whole
+ *              128-B lines of its tile.  The g(T) and FTRL-vs-exact entry points also
  *              take the closed-form comparator losses in this mode wherever the kernel
  *              certifies them (ocx_dev_simulate_alg_ex), so their results are NOT
  *              bit-identical to the reference: the loops keep the sums above, the

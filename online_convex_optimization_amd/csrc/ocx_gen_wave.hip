@@ -39,6 +39,10 @@ constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 #ifndef OCX_GEN_WEDGE_F32
 #define OCX_GEN_WEDGE_F32 0
 #endif
+// WU (zig_round): the wedge test of a rejection round on every lane, its outcome read off
+// ballots (no exec-mask branches, no per-lane bool carried into the parse).  Bit-identical;
+// the d = 1024 rows take it (2 048 x 1e4: 77.2 / 77.5 -> 76.2 / 76.0 ms), the d = 64 rows
+// measured slower with it (58.9 -> 60.5 ms; profiles/r03_gen_wu_ab.jsonl).
 
 // The fast path's table lookup (ki[idx], wi[idx] for a random layer idx per lane) is one
 // ds_read_b128 of an interleaved {ki, wi} entry: the two separate tables read as a
@@ -373,7 +377,8 @@ __device__ __forceinline__ unsigned rix(unsigned i) {
 
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.  SW: the ring's slot map (rix).
-template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0, bool KD = false>
+template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0, bool WU = false,
+          bool KD = false>
 __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, double* ring, int rmask,
                          unsigned head, int lane) {
     const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
@@ -468,6 +473,25 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
     if (rej) {
         // wedge test of a rejected draw k uses draw k+1 (next_double) as its uniform
         const uint64_t rn = shfl_down1(r);
+        uint64_t tailm;
+        if constexpr (WU && !OCX_GEN_WEDGE_F32) {
+            // the same double arithmetic on every lane; lanes that are not wedge candidates
+            // compute values nobody reads, from a valid table row
+            const uint64_t zidx = ballot(idx == 0);
+            const uint64_t cm = rej & ~zidx;  // wedge candidates
+            tailm = rej & zidx;               // tail draws (layer 0)
+            const int i1 = idx ? idx : 1;
+            const double lhs = (tb.fi[i1 - 1] - tb.fi[i1]) * u53(rn) + tb.fi[i1];
+            const double a = -0.5 * x * x;
+            const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
+            wacc = cm & ballot(lhs < e * (1.0 - 1e-5));
+            const uint64_t unsure = cm & ~wacc & ~ballot(lhs > e * (1.0 + 1e-5));
+            if (unsure) {  // ~1e-5 of wedge tests: NumPy's exact comparison
+                bool ex = false;
+                if ((unsure >> lane) & 1) ex = wedge_exact(lhs, a);
+                wacc |= ballot(ex);
+            }
+        } else {
         bool wa = false;
 #ifdef OCX_GEN_TUNE_NO_WEDGE  // tuning only: no wedge test (wrong normals)
         if (false) {
@@ -506,7 +530,8 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
         }
 #endif
         wacc = ballot(wa);
-        const uint64_t tailm = ballot(!fast && idx == 0);
+        tailm = ballot(!fast && idx == 0);
+        }
         // Usual case: no tail draw and no two rejected draws side by side, so every
         // rejected draw k takes draw k+1 as its uniform and a rejected draw 63 is redone
         // next round: the walk below reduces to two bit operations.
@@ -978,7 +1003,7 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
 #if OCX_GEN_INNER
                 if (total - produced >= 1024u + 64u) {  // a whole row still to draw
                     do {
-                        const int n = zig_round<true, true, kF1k, kSW>(w, 64, tb, ring, kFlat, head, lane);
+                        const int n = zig_round<true, true, kF1k, kSW, true>(w, 64, tb, ring, kFlat, head, lane);
                         produced += (uint32_t)n;
                         head += (unsigned)n;
                     } while (head < 1024u);
@@ -987,8 +1012,8 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
                 {
                     const uint32_t left = total - produced;
                     const int n = left >= 64u
-                                      ? zig_round<true, true, kF1k, kSW>(w, 64, tb, ring, kFlat, head, lane)
-                                      : zig_round<true, false, kF1k, kSW>(w, (int)left, tb, ring,
+                                      ? zig_round<true, true, kF1k, kSW, true>(w, 64, tb, ring, kFlat, head, lane)
+                                      : zig_round<true, false, kF1k, kSW, true>(w, (int)left, tb, ring,
                                                                          kFlat, head, lane);
                     produced += (uint32_t)n;
                     head += (unsigned)n;

@@ -12,10 +12,11 @@ Two ways in:
 
 Every batched call defaults to ``lanes_per_seq=LANES_BEST`` (include/ocx.h,
 OCX_LANES_BEST), the fastest certified mode: the exact layout's sequential sums wherever its
-lane chains are short and the kernels stream at the HBM roofline (e.g. d=64 with >= 8192
-sequences per batch, every d <= 16 batch), butterfly sums (~1e-16 relative) where an exact
-chain of 8+ lanes would leave the kernel latency-bound (d >= 512, few-wave batches such as
-the capacity-limited T=1e5 g(T) batch), and — for the g(T), DeviceBatch and FTRL-vs-exact
+lane chains are short and d < 64 (every d <= 16 batch, the drivers' d=5 batches), butterfly
+sums (~1e-16 relative) where an exact chain of 8+ lanes would leave the kernel latency-bound
+(d >= 512, few-wave batches such as the capacity-limited T=1e5 g(T) batch) and for batches
+of >= 4096 sequences at 64 <= d <= 128 (the pipelined 8 x 8 kernel: the bench's 32 768 x 1e4
+batch), and — for the g(T), DeviceBatch and FTRL-vs-exact
 paths — the closed-form comparator losses wherever the kernel certifies them (one HBM pass
 instead of two; about 1e-13 relative on the regret).  LANES_BEST results are therefore NOT
 bit-identical to the reference.  ``lanes_per_seq=1`` forces the bit-exact mode (sequential

@@ -1,16 +1,15 @@
 #!/bin/bash
-# Round 3: generator correctness (the device-generator parity tests on the default build)
-# and A/B timings of the generator variants in tune_r03/ (built in the container).
+# Round 3: generator A/B — the libraries in tune_r03/ named by $1 (comma-separated, the
+# first the reference) run the generator parity tests' shapes for bit identity, then timings
+# twice (forward and reversed order), on one box.
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "generator or gT or families or published or full_size or config" -x -v --timeout 180 --timeout-method thread > gpurun_out/pytest_gen.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gen.log; exit 2; }
-tail -2 gpurun_out/pytest_gen.log
-timeout -k 10 300 python -u tools/tune_gen.py --dir tune_r03 --variants old,f32only,speconly,cheapmul --rounds 3 > gpurun_out/r03_gen_ab.jsonl 2> gpurun_out/r03_gen_ab.err || { echo "ab failed"; tail -20 gpurun_out/r03_gen_ab.err; exit 3; }
-cat gpurun_out/r03_gen_ab.jsonl
-timeout -k 10 300 python -u tools/tune_gen.py --dir tune_r03 --variants old --B 4900 --T 100000 --lanes 128 --rounds 2 >> gpurun_out/r03_gen_ab.jsonl 2>> gpurun_out/r03_gen_ab.err || { echo "ab2 failed"; exit 4; }
-tail -2 gpurun_out/r03_gen_ab.jsonl
-timeout -k 10 600 python -u -m pytest tests/test_gpu_smart.py -x -v --timeout 180 --timeout-method thread > gpurun_out/pytest_smart.log 2>&1 || { echo "smart pytest failed"; tail -40 gpurun_out/pytest_smart.log; exit 5; }
-tail -2 gpurun_out/pytest_smart.log
-timeout -k 10 600 python -u tools/r03_smart_probe.py > gpurun_out/r03_smart_probe.jsonl 2>gpurun_out/r03_smart_probe.err || { echo "probe failed"; tail -20 gpurun_out/r03_smart_probe.err; exit 6; }
-cat gpurun_out/r03_smart_probe.jsonl
+LIBS="$1"; OUT="gpurun_out/$2"
+REV=$(echo "$LIBS" | tr ',' '\n' | tac | paste -sd,)
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "generator" -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gen.log 2>&1 || { echo "gen pytest failed"; tail -40 gpurun_out/pytest_gen.log; exit 2; }
+tail -1 gpurun_out/pytest_gen.log
+timeout -k 10 400 python -u tools/r03_gen_lib_ab.py "$LIBS" > "$OUT" 2> "$OUT.err" || { echo "ab failed"; tail -20 "$OUT.err"; exit 3; }
+timeout -k 10 400 python -u tools/r03_gen_lib_ab.py "$REV" >> "$OUT" 2>> "$OUT.err" || { echo "ab2 failed"; tail -20 "$OUT.err"; exit 4; }
+grep -v '"what"' "$OUT" | sort | uniq -c
+grep ms_min "$OUT" | cut -c1-120
