@@ -311,7 +311,7 @@ def main():
             pass
         cpu = None
         parity = None
-        if a.cpu_seconds > 0:
+        if a.cpu_seconds > 0 and world == 1:  # the CPU leg: rank 0 at N = 1 only
             cregs, cps, spent = cpu_baseline(T, d, B, a.cpu_seconds)
             err = np.abs(regrets[:len(cregs)] - cregs)
             # the closed-form comparator differs from the reference's sequential sum by

@@ -1,7 +1,7 @@
 // ocx_gen_wave.hip — the g(T) adversary (fast_algorithms.py:231-239) with one
 // wavefront per NumPy stream.
 //
-// NumPy's ziggurat is sequential per stream, but 99.3 % of its draws are accepted on
+// NumPy's ziggurat is sequential per stream, but 98.5 % of its draws are accepted on
 // the fast path, so a wave speculates: lane k computes raw draw k of the stream by
 // PCG64 jump-ahead (state_{n+k+1} = A^{k+1} state_n + inc·(A^k + … + 1)), runs the
 // fast test, and the wave then parses the 64 draws in stream order.  A rejected draw
@@ -377,10 +377,33 @@ __device__ __forceinline__ unsigned rix(unsigned i) {
 
 // FLAT: the ring is never wrapped (the caller keeps head + 64 within it and moves what is
 // left to the front itself): ring indices go unmasked.  SW: the ring's slot map (rix).
+// DF (deferred wedges, the d = 64 rows' full rounds; OCX_GEN_DEFER): a round does not run
+// the wedge test of its rejected draws.  Whatever the test decides, a rejected draw k < 63
+// consumes draw k+1 as its uniform, so the draws a full round consumes — and the stream
+// state — do not depend on it; only whether x_k is emitted does.  The round emits every
+// candidate tentatively and appends {ring slot, layer, next draw} to the wave's pending list;
+// resolve_wedges() runs the tests of the whole list at once (one wave instruction per
+// operation for all of them, instead of one per rejected draw) and compacts the ring where a
+// test rejects, before anything reads the ring's rows.  Bit-identical, and measured slower:
+// 32 768 x 1e4 x 64 took 69.6 vs 58.9 ms (profiles/r03_gen_defer_ab.jsonl).  With NumPy's
+// tables 46 % of wedge tests reject, so nearly every batch compacts its ring (~3.6 slots),
+// and the compaction's read -> ballot -> write chain per 64-slot chunk is latency the four
+// waves per SIMD do not hide; the ~22 VALU per rejection round it saves are less.  Off; a
+// tuning knob.
+#ifndef OCX_GEN_DEFER
+#define OCX_GEN_DEFER 0
+#endif
+// A round's candidates are attempts, never adjacent draws (an attempt consumes the next draw)
+// and never draw 63: at most 32 per round.  Resolving once 32 are pending keeps the list
+// within one wavefront (<= 63 entries).
+constexpr int kPendMax = 64;    // pending entries per wave
+constexpr int kPendFlush = 32;  // resolve once this many are pending
+
 template <bool RING, bool FULL = false, bool FLAT = false, int SW = 0, bool WU = false,
-          bool KD = false>
-__device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, double* ring, int rmask,
-                         unsigned head, int lane) {
+          bool DF = false, bool KD = false>
+__device__ __attribute__((always_inline)) int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, double* ring, int rmask,
+                         unsigned head, int lane, uint64_t* pend = nullptr, int* npend = nullptr) {
+    static_assert(!DF || (FULL && FLAT), "deferred wedges: full rounds of the flat ring only");
     const unsigned fmask = FLAT ? ~0u : (unsigned)rmask;
     constexpr bool LS = FLAT && OCX_GEN_LANE_STATE;  // lane states (d = 64 rows)
 #if OCX_GEN_SPEC_NEXT
@@ -418,7 +441,7 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
     else fast = rabs < kidx;
 #endif
     const uint64_t rej = ballot(!fast);
-    if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (64 % of rounds)
+    if (rej == 0 && (FULL || need == 64)) {  // every draw accepted (38 % of rounds)
         if (RING) ring[rix<SW>((head + (unsigned)lane) & fmask)] = x;
 #if OCX_GEN_SPEC_NEXT
         w.base = s63;
@@ -470,11 +493,17 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
 #endif
     uint64_t cons = 0, wacc = 0;
     int limit = 64, tail_k = -1;
+    uint64_t rn = 0;
     if (rej) {
         // wedge test of a rejected draw k uses draw k+1 (next_double) as its uniform
-        const uint64_t rn = shfl_down1(r);
+        rn = shfl_down1(r);
         uint64_t tailm;
-        if constexpr (WU && !OCX_GEN_WEDGE_F32) {
+        if constexpr (DF) {
+            // every wedge candidate tentatively accepted (resolve_wedges decides)
+            const uint64_t zidx = ballot(idx == 0);
+            tailm = rej & zidx;
+            wacc = rej & ~zidx;
+        } else if constexpr (WU && !OCX_GEN_WEDGE_F32) {
             // the same double arithmetic on every lane; lanes that are not wedge candidates
             // compute values nobody reads, from a valid table row
             const uint64_t zidx = ballot(idx == 0);
@@ -575,6 +604,17 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
         tail_k = -1;
     }
     if (RING && ((emit >> lane) & 1)) ring[rix<SW>((head + mbcnt(emit)) & fmask)] = x;
+    if constexpr (DF) {
+        const uint64_t pc = emit & rej;  // tentatively emitted wedge candidates
+        if (pc) {
+            if ((pc >> lane) & 1) {
+                uint64_t* e = pend + 2 * (*npend + mbcnt(pc));
+                e[0] = (uint64_t)(head + (unsigned)mbcnt(emit)) | ((uint64_t)(uint32_t)idx << 32);
+                e[1] = rn;
+            }
+            *npend += __builtin_popcountll(pc);
+        }
+    }
     if (tail_k >= 0) {
         // NumPy's tail loop, sequential from the state after the tail draw
         const ocx_u128 st = rl128(s, tail_k);
@@ -609,6 +649,56 @@ __device__ int zig_round(WaveStream& w, int need, const ZigTables<KD>& tb, doubl
         w.s = m == 64 ? mul_add_u128(s, kA64, w.C64v) : mul_add_u128(w.Ak, rl128(s, m - 1), w.Dk);
 #endif
     return n;
+}
+
+// The wedge tests of the pending list (see DF above), all at once: lane i tests entry i, in
+// NumPy's double arithmetic (the 1e-5 float-estimate margin, the exact comparison where too
+// close to call).  Each rejected entry's slot is removed from the flat ring (flags in `gone`,
+// one byte per slot: every later normal moves down by the removed slots before it), and
+// head / produced drop by the count.  Pending entries are in stream order, so are slots.
+template <bool KD>
+__device__ __forceinline__ void resolve_wedges(double* ring, const uint64_t* pend, unsigned char* gone,
+                                               int& npend, unsigned& head, uint32_t& produced,
+                                               const ZigTables<KD>& tb, int lane) {
+    if (npend == 0) return;
+    const bool act = lane < npend;
+    uint64_t w0 = 1ULL << 32, rn = 0;  // inactive lanes: layer 1, slot 0 (read, never used)
+    if (act) {
+        w0 = pend[2 * lane];
+        rn = pend[2 * lane + 1];
+    }
+    const unsigned pos = (unsigned)w0;
+    const int idx = (int)(w0 >> 32);
+    const double x = ring[pos];
+    const double lhs = (tb.fi[idx - 1] - tb.fi[idx]) * u53(rn) + tb.fi[idx];
+    const double a = -0.5 * x * x;
+    const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
+    const uint64_t am = lowmask(npend);
+    uint64_t accm = am & ballot(lhs < e * (1.0 - 1e-5));
+    const uint64_t un = am & ~accm & ~ballot(lhs > e * (1.0 + 1e-5));
+    if (un) {  // ~1e-5 of wedge tests
+        bool ex = false;
+        if ((un >> lane) & 1) ex = wedge_exact(lhs, a);
+        accm |= ballot(ex);
+    }
+    npend = 0;
+    const uint64_t rejm = am & ~accm;
+    if (rejm == 0) return;
+    const bool rj = (rejm >> lane) & 1;
+    if (rj) gone[pos] = 1;
+    const unsigned first = (unsigned)__builtin_amdgcn_readlane((int)pos, __builtin_ctzll(rejm));
+    unsigned before = 0;  // removed slots below the current chunk
+    for (unsigned c = first & ~63u; c < head; c += 64) {
+        const unsigned j = c + (unsigned)lane;
+        const bool in = j < head;
+        const double v = in ? ring[j] : 0.0;
+        const uint64_t gm = ballot(in && gone[j] != 0);
+        if (in && !((gm >> lane) & 1)) ring[j - before - (unsigned)mbcnt(gm)] = v;
+        before += (unsigned)__builtin_popcountll(gm);
+    }
+    if (rj) gone[pos] = 0;
+    head -= before;
+    produced -= before;
 }
 
 // NumPy pairwise sum of v*v over one leaf of n <= 128 ring values starting at o.
@@ -793,6 +883,7 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
     constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && (DF == 64 || (DF == 1024 && OCX_GEN_1K_FLAT));
     constexpr bool kKD = OCX_GEN_KI_DOUBLE && DF == 64;  // ki as doubles (see ZigTables)
+    constexpr bool kDF = OCX_GEN_DEFER && MODE == 0 && DF == 64 && !LR && OCX_GEN_INNER;  // deferred wedges
     __shared__ ZigTables<kKD> tb;
     extern __shared__ double rings[];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -812,6 +903,10 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
     double* ring = rings + (threadIdx.x >> 6) * slot;
     PwFrame* stk = reinterpret_cast<PwFrame*>(ring + rb);
     const int rmask = rb - 1;
+    if constexpr (kDF) {  // the removed-slot flags start clear (resolve_wedges clears its own)
+        unsigned char* gone = reinterpret_cast<unsigned char*>(ring + kRows64 * 64 + 64 + 8 + 2 * kPendMax);
+        for (int i = lane; i < kRows64 * 64 + 64; i += 64) gone[i] = 0;
+    }
 
     // jump-ahead constants of this lane: A^(k+1) and A^k + ... + A + 1
     WaveStream w;
@@ -930,25 +1025,35 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
             unsigned head = 0;  // normals in the ring
             int64_t t = 0;
             double* scl = ring + RR * 64 + 64;  // the batch's row scales
+            // deferred wedges (the default form): the pending list and the removed-slot flags
+            // follow the scales in the wave's slot (ring_doubles)
+            uint64_t* pend = reinterpret_cast<uint64_t*>(ring + RR * 64 + 64 + 8);
+            unsigned char* gone = reinterpret_cast<unsigned char*>(ring + RR * 64 + 64 + 8 + 2 * kPendMax);
+            int npend = 0;
             while (produced < total) {
 #if OCX_GEN_INNER
                 if (total - produced >= (uint32_t)(RR * 64 + 64)) {
                     // a whole batch still to draw: full rounds until the ring holds it, with
                     // one loop test per round (no per-round need / last-round / batch tests;
-                    // every round here has 64 or more normals left to draw)
+                    // every round here has 64 or more normals left to draw — with deferred
+                    // wedges `produced` may count tentative normals, so the true remainder is
+                    // larger still)
                     do {
-                        const int n = zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane);
+                        const int n = zig_round<true, true, true, 0, false, kDF>(w, 64, tb, ring, 0, head,
+                                                                                lane, pend, &npend);
                         produced += (uint32_t)n;
                         head += (unsigned)n;
 #if OCX_GEN_UNROLL == 2
                         // two rounds per trip: the state alternates between two register sets
                         // (no back-edge copies of the 128-bit lane states)
-                        if (head >= (unsigned)(RR * 64)) break;
-                        const int n2 = zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane);
+                        if (head >= (unsigned)(RR * 64) || (kDF && npend >= kPendFlush)) break;
+                        const int n2 = zig_round<true, true, true, 0, false, kDF>(w, 64, tb, ring, 0, head,
+                                                                                 lane, pend, &npend);
                         produced += (uint32_t)n2;
                         head += (unsigned)n2;
 #endif
-                    } while (head < (unsigned)(RR * 64));
+                    } while (head < (unsigned)(RR * 64) && !(kDF && npend >= kPendFlush));
+                    if constexpr (kDF) resolve_wedges(ring, pend, gone, npend, head, produced, tb, lane);
                 } else
 #endif
                 {
@@ -1208,7 +1313,10 @@ namespace {
 
 int ring_doubles(int64_t d, int DF, bool LR = false) {
     if (DF == 1024) return 1024 + 64;  // one row + the next row's first round (ocx_gen_wave_kernel)
-    if (DF == 64) return kRows64 * 64 + 64 + 8;  // R rows + one round, then the R row scales
+    // R rows + one round, the R row scales; the default form also the deferred-wedge list
+    // (kPendMax 16-B entries) and one flag byte per ring slot
+    if (DF == 64)
+        return kRows64 * 64 + 64 + 8 + ((OCX_GEN_DEFER && !LR) ? 2 * kPendMax + (kRows64 * 64 + 64) / 8 : 0);
     // a full batch of rows plus one round of normals
     int rb = 128;
     while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
