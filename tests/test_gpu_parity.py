@@ -399,11 +399,14 @@ def test_streamed_gT_matches_resident(ocx, monkeypatch, T, d, runs, P):
 
 @pytest.mark.parametrize("T,d,runs,exact", [(200, 64, 700, False), (60, 64, 9000, False),
                                              (60, 32, 9000, True), (40, 1024, 40, False),
-                                             (300, 5, 500, True)])
+                                             (300, 5, 500, True), (50, 16, 5000, True),
+                                             (40, 8, 3000, True)])
 def test_best_mode_default(ocx, T, d, runs, exact):
     """The batched APIs' default (OCX_LANES_BEST): the exact layout's sums where its chains
     are short — d < 64 — and butterfly sums for d=64 batches (the pipelined kernel: few-wave
-    and big ones alike) and d=1024, with the certified closed-form comparator in both cases, so the
+    and big ones alike) and d=1024, with the certified closed-form comparator in both cases
+    (the g(T) entry points, which generate their batches, take butterfly lanes of two
+    coordinates for 8 <= d < 64, ocx_capi.hip gT_run), so the
     default is held to close_closed against the oracle, never to bit equality (the
     bit-exact mode, lanes_per_seq=1, is checked bit for bit beside it)."""
     eng, lib = ocx["engine"], ocx["lib"]

@@ -4,6 +4,7 @@
   sweep    configs[3]-style g(T) sweep per T, generation included (runs scaled down)
   driver   fast_driver.main() on device (g(T) runs=1000 + the four cases, full sizes)
   smart    SMART kernel throughput (d=5, T=1000, 768 sequences)
+  config1  configs[1] (65 536 x 1e3 x 16) per lanes_per_seq layout
 """
 import argparse
 import json
@@ -225,6 +226,54 @@ def exact_driver(args):
                                 for t, st in stats.items()}}), flush=True)
 
 
+def config1(args):
+    """configs[1]: batched FTRL, 65 536 sequences, d=16, T=1e3 (g(T) adversary at d=16),
+    per layout: kernel time from HIP events, fraction of 8 TB/s for one and two passes over z,
+    generation time, and regrets against the exact layout."""
+    import torch
+    from online_convex_optimization_amd import engine
+    B, T, d = 65536, 1000, args.d
+    ref = None
+    for lanes in [int(v) for v in args.lanes_list.split(",")]:
+        db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes)
+        st = torch.cuda.current_stream()
+        db.generate_gT(0, 0)
+        sync()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(st)
+        db.generate_gT(0, 0)
+        ev[1].record(st)
+        db.simulate_alg()
+        ev[2].record(st)
+        sync()
+        res = []
+        for closed in (True, False):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            db.simulate_alg(closed_comparator=closed)
+            e0.record(st)
+            for _ in range(10):
+                db.simulate_alg(closed_comparator=closed)
+            e1.record(st)
+            sync()
+            res.append(e0.elapsed_time(e1) / 10)
+        r = db.regret[:B].cpu().numpy()
+        if ref is None and db.exact:
+            ref = r.copy()
+        err = None if ref is None else float(np.max(np.abs(r - ref) / np.maximum(1, np.abs(ref))))
+        one, two = B * T * (8 * d + 8), 2 * B * T * (8 * d + 8)
+        print(json.dumps({"what": "config1", "d": d, "lanes": lanes, "layout": [db.L.P, db.L.C, db.L.chain],
+                          "exact": bool(db.exact), "gen_ms": ev[0].elapsed_time(ev[1]),
+                          "ftrl_ms_default": ev[1].elapsed_time(ev[2]),
+                          "ftrl_ms_closed": res[0], "ftrl_ms_two_pass": res[1],
+                          "frac_closed": one / (res[0] * 1e-3) / 8e12,
+                          "frac_two_pass": two / (res[1] * 1e-3) / 8e12,
+                          "timesteps_per_s_closed": B * T / (res[0] * 1e-3),
+                          "max_rel_vs_exact": err}), flush=True)
+        del db
+        engine.release_buffers()
+        torch.cuda.empty_cache()
+
+
 def smart(args):
     """SMART on the driver's batch shape (768 iid sequences, d=5, T=1000) and a large
     batch, through both kernels (OCX_SMART_KERNEL=lanes|wave)."""
@@ -257,7 +306,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--lanes", type=int, default=128, help="lanes_per_seq of the sweeps")
     ap.add_argument("--Ts", default="", help="sweep: only these horizons (comma list)")
-    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config3", "exact_driver", "config4", "sweep_budget", "prof_long"])
+    ap.add_argument("--d", type=int, default=16, help="config1: the dimension")
+    ap.add_argument("--lanes-list", default="128,1,0,2,4,-2,-4", help="config1: layouts to time")
+    ap.add_argument("what", nargs="+", choices=["gen", "gen1", "sweep", "driver", "smart", "config1", "config3", "exact_driver", "config4", "sweep_budget", "prof_long"])
     a = ap.parse_args()
     for w in a.what:
         globals()[w](a)
