@@ -793,9 +793,10 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
     // two lanes per sequence leave each generator wave (one stream) writing 16- or 32-B
     // pieces of a row into C/2 planes of the tile.  OCX_LANES_BEST takes butterfly lanes of
     // two coordinates here, up to 8 lanes (128-B row pieces): 65 536 x 1e3, generation +
-    // FTRL: d = 16 27.6 -> 7.5 ms, d = 32 21.7 -> 12.7, d = 8 14.1 -> 4.8 (the FTRL kernel
-    // alone 1.36 -> 1.60 ms at d = 16; profiles/r03_config1_layouts.jsonl).
-    if (lanes_per_seq == OCX_LANES_BEST && d >= 8 && d < 64) lanes_per_seq = d >= 16 ? 8 : 4;
+    // FTRL: d = 16 27.6 -> 7.5 ms, d = 32 21.7 -> 12.7, d = 8 14.1 -> 4.8, d = 5 (two
+    // lanes) 10.6 -> 7.9 (the FTRL kernel alone 1.36 -> 1.60 ms at d = 16;
+    // profiles/r03_config1_layouts.jsonl, r03_gt_small_d.jsonl).
+    if (lanes_per_seq == OCX_LANES_BEST && d >= 4 && d < 64) lanes_per_seq = d >= 16 ? 8 : (d >= 8 ? 4 : 2);
     DevCtx* cx;
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);

@@ -406,7 +406,7 @@ def test_best_mode_default(ocx, T, d, runs, exact):
     are short — d < 64 — and butterfly sums for d=64 batches (the pipelined kernel: few-wave
     and big ones alike) and d=1024, with the certified closed-form comparator in both cases
     (the g(T) entry points, which generate their batches, take butterfly lanes of two
-    coordinates for 8 <= d < 64, ocx_capi.hip gT_run), so the
+    coordinates for 4 <= d < 64, ocx_capi.hip gT_run), so the
     default is held to close_closed against the oracle, never to bit equality (the
     bit-exact mode, lanes_per_seq=1, is checked bit for bit beside it)."""
     eng, lib = ocx["engine"], ocx["lib"]

@@ -14,7 +14,7 @@ def main():
     import numpy as np
     from online_convex_optimization_amd import engine
     T, runs = 1000, 65536
-    for d in (8, 16, 32):
+    for d in (5, 8, 16, 32):
         ref = None
         for name, lanes in (("best", engine.LANES_BEST), ("exact", 1)):
             engine.gT_regrets(T, 4096, base_seed=0, d=d, lanes_per_seq=lanes)  # warm up
