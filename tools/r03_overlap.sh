@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round 3: generation of batch k+1 beside the FTRL pass over batch k (two streams, double
 # buffered; tools/overlap2.py) with the pipelined 8 x 8 kernel, plain and with the FTRL waves
-# at issue priority 3 (OCX_ALG_PRIO build).
+# at issue priority 3.  Needs tune_r03/libocx_prio3.so: _build.build_variant("prio3",
+# ["OCX_ALG_PRIO=3"], source="ocx_alg_pipe.hip", out_dir="tune_r03").
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"; mkdir -p gpurun_out
