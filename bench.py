@@ -163,6 +163,47 @@ def host_cpu():
             "nproc": os.cpu_count(), "affinity": aff}
 
 
+def device_identity(gpu: int) -> dict:
+    """Which physical GPU this rank drives: torch's device index, the PCI location and the
+    UUID from the HIP device properties, and the visibility masks the launcher set."""
+    import torch
+    p = torch.cuda.get_device_properties(gpu)
+    pci = [getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id")]
+    ident = {"device_index": int(gpu), "name": getattr(p, "name", None),
+             "pci": None if None in pci else "%04x:%02x:%02x" % tuple(int(v) for v in pci),
+             "uuid": str(getattr(p, "uuid", "")) or None}
+    for k in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        if os.environ.get(k) is not None:
+            ident[k] = os.environ[k]
+    return ident
+
+
+def rank_report(dist, rank: int, world: int, ident: dict, elapsed_s: float, kern_ms: float,
+                regrets: np.ndarray, gathered: np.ndarray) -> dict:
+    """The multi-rank self-check printed with the bench line (collective: every rank calls
+    it).  Every rank contributes its identity, its own wall time over the timed steps, its
+    kernel time and a checksum of its own regrets (all_gather_object); rank 0 then checks
+    each rank's block of the gathered regret vector against that rank's checksum, so the
+    line shows that N distinct GPUs ran N disjoint shards and that the collective moved
+    them intact."""
+    regrets = np.asarray(regrets, dtype=np.float64)
+    mine = dict(ident, rank=int(rank), elapsed_ms=float(elapsed_s) * 1e3,
+                kernel_ms=float(kern_ms), n_regrets=int(regrets.size),
+                regret_sum=float(np.sum(regrets)), regret_sumsq=float(np.sum(regrets * regrets)))
+    rows = [None] * world
+    dist.all_gather_object(rows, mine)
+    B = regrets.size
+    g = np.asarray(gathered, dtype=np.float64)
+    blocks_ok = [g.size == world * B
+                 and float(np.sum(g[r * B:(r + 1) * B])) == rows[r]["regret_sum"]
+                 and float(np.sum(g[r * B:(r + 1) * B] ** 2)) == rows[r]["regret_sumsq"]
+                 for r in range(world)]
+    keys = [(r.get("pci") or r.get("uuid") or f"index{r['device_index']}") for r in rows]
+    return {"world_size": int(dist.get_world_size()), "ranks": rows,
+            "distinct_devices": len(set(keys)), "gathered_check": bool(all(blocks_ok)),
+            "gathered_blocks_ok": blocks_ok}
+
+
 def main():
     a = parse()
     import torch
@@ -291,6 +332,13 @@ def main():
                        "the pipeline's traffic: the generator's write and one FTRL read)"}
 
     regrets = db.regret[:B].cpu().numpy()
+    ranks = None
+    if dist_on:
+        # the regret vector of the last timed step (the e2e batches regenerate the same runs)
+        gather()
+        torch.cuda.synchronize()
+        ranks = rank_report(dist, rank, world, device_identity(gpu), elapsed, kern_ms, regrets,
+                            gathered.cpu().numpy())
     out = None
     if rank == 0:
         steps_per_launch = B * T
@@ -392,9 +440,11 @@ def main():
             "gen_timesteps_per_s": B * T / gen_s,
         }
         if dist_on:
-            g = gathered.cpu().numpy()
-            out["gathered_check"] = bool(np.array_equal(g[:B], regrets))
             out["dist_backend"] = a.dist_backend
+            out["world_size"] = ranks["world_size"]
+            out["distinct_devices"] = ranks["distinct_devices"]
+            out["gathered_check"] = ranks["gathered_check"]
+            out["ranks"] = ranks["ranks"]
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.barrier()

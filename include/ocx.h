@@ -51,7 +51,15 @@
  * ocx_ftrl_vs_exact_batch has its round-1 signature again (the `norm` argument moved to
  * ocx_ftrl_vs_exact_batch_ex); callers built against 0.1.x check ocx_version() >= 200.
  * 0.3.0 adds the general exact-FTL solver (ocx_exact_ball_solve, ocx_dev_exact_ball_solve,
- * ocx_dev_exact_ball_solve_tiled); nothing existing changed. */
+ * ocx_dev_exact_ball_solve_tiled); nothing existing changed.
+ *
+ * Checking the ABI: one intermediate 0.1.x tree exported ocx_ftrl_vs_exact_batch WITH a
+ * `norm` argument under the same symbol and the same version number as the release without
+ * it, so a version number alone cannot tell those two apart and a C linker will not either.
+ * A C caller must therefore require EXACT equality, ocx_version() == the OCX_VERSION it was
+ * compiled with (OCX_ABI_MATCHES() below), not ocx_version() >= some minimum, and must take
+ * `norm` through ocx_ftrl_vs_exact_batch_ex only.  The Python binding (_lib.py) checks
+ * equality the same way. */
 #define OCX_VERSION 300
 
 #include <stddef.h>
@@ -92,6 +100,8 @@ typedef struct ocx_layout {
 
 /* ---- library / device ---------------------------------------------------- */
 int ocx_version(void);
+/* 1 when the loaded library implements exactly the ABI this header describes. */
+#define OCX_ABI_MATCHES() (ocx_version() == OCX_VERSION)
 int ocx_last_error(char* buf, size_t len);
 int ocx_device_count(int* count);
 /* Free the HBM the library caches per device for its host entry points and g(T) sweeps

@@ -116,7 +116,11 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_closed_kernel(
                 } else {
                     total_loss += lf;  // :156
                     bool decided = false, fire = false;
-                    if (closed_prefix && regime) {
+                    if (closed_prefix && ftl_loss < th_sw) {
+                        // s_loss >= 0, so fl(ftl_loss - s_loss) <= ftl_loss < thresh: the
+                        // reference's test is false whatever the prefix (any thresh, +inf too)
+                        decided = true;
+                    } else if (closed_prefix && regime) {
                         double p[C];
 #pragma unroll
                         for (int j = 0; j < C; ++j) p[j] = xf[j] * sv[j];
@@ -124,10 +128,17 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_smart_closed_kernel(
                         const double n1 = (double)(t + 1);
                         const double s_cl = 0.5 * n1 - 0.5 * dot;
                         const double D = ftl_loss - s_cl - th_sw;
+                        // an infinite threshold must not widen the band (+inf: never fires,
+                        // D = -inf; -inf: fires at once, D = +inf), and a NaN one never fires
+                        // (`>= NaN` is false, :159) — decided here, not by O(t) re-scans
+                        const double tha = __builtin_isfinite(th_sw) ? fabs(th_sw) : 0.0;
                         const double guard =
                             n1 * (1e-12 + 2.5e-16 * (2.0 * n1 + 2.0 * (double)d + 8.0)) +
-                            4e-16 * (fabs(ftl_loss) + n1 + fabs(th_sw));
-                        if (fabs(D) > guard) {  // NaN thresholds fall through to the re-scan
+                            4e-16 * (fabs(ftl_loss) + n1 + tha);
+                        if (th_sw != th_sw) {
+                            decided = true;
+                            fire = false;
+                        } else if (fabs(D) > guard) {
                             decided = true;
                             fire = D > 0.0;
                         }

@@ -18,7 +18,8 @@ kernel implements) reproduces every value bit for bit, and stores inputs and out
 * ``smart_*``      — SMART with thresholds that switch early, late and never;
 * ``dim{d}_*``     — d in {1, 2, 8, 16, 31} (the host BLAS orders sgemv differently for
                      some of them; the GPU is held to a tolerance there);
-* ``gT_*``         — the twin's g(T) sampler and its thresholds (runs 0..15).
+* ``gT_*``         — the twin's g(T) sampler and its thresholds (runs 0..15);
+* ``cfg0_*``       — BASELINE configs[0]: d = 2, T = 1000 (an i.i.d. stream, a g(T) sample).
 """
 from __future__ import annotations
 
@@ -196,6 +197,12 @@ def main():
             regs[r] = np_simulate_alg(z, y, 0, math.sqrt(2))[0]
             assert regs[r] == O.t32_simulate_alg_full(zo, yo, 0, math.sqrt(2))[0]
         out[f"gT_T{T}_regrets"] = regs
+    # BASELINE configs[0]: driver.py's single FTL run, d = 2, T = 1000, one random sequence
+    # (the i.i.d. family of sequence_generation.py:54-69 at d = 2, and one g(T) sample)
+    zc, yc, _ = O.random_iid_sample(2025, 1000, 0, d=2)
+    zg, yg = np_gT_sample(1000, 0, d=2)
+    _alg_group(out, "cfg0", np.stack([np.asarray(zc, F), zg]), np.stack([np.asarray(yc, F), yg]),
+               runs)
     grid = [100, 200, 300]
     g = O.t32_empirical_worst_case_thresholds(grid, runs=8)
     out["gT_grid"] = np.array(grid, np.int64)

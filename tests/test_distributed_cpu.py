@@ -43,6 +43,56 @@ def _worker(rank, world, port, T_grid, runs, q):
     dist.destroy_process_group()
 
 
+def _bench_report_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 5
+    regrets = np.random.default_rng(rank).standard_normal(B)
+    gathered = torch.zeros(world * B, dtype=torch.float64)
+    dist.all_gather_into_tensor(gathered, torch.from_numpy(regrets))
+    ident = {"device_index": rank, "name": "cpu-stand-in", "pci": f"0000:{rank + 0x10:02x}:00",
+             "uuid": None}
+    rep = bench.rank_report(dist, rank, world, ident, 0.25 + rank, 1.5, regrets,
+                            gathered.numpy())
+    bad = gathered.numpy().copy()
+    bad[-1] += 1.0  # the last rank's block corrupted
+    rep_bad = bench.rank_report(dist, rank, world, ident, 0.25, 1.5, regrets, bad)
+    q.put((rank, rep, rep_bad["gathered_check"], rep_bad["gathered_blocks_ok"]))
+    dist.destroy_process_group()
+
+
+def test_bench_rank_report_world2():
+    """bench.py's multi-rank self-check (what the 8-GPU SCALE run prints): world size,
+    every rank's device identity, wall time and kernel time, and a gathered_check that
+    compares every rank's block of the gathered regrets with that rank's own checksum."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_bench_report_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, rep, bad_ok, bad_blocks = q.get(timeout=300)
+        res[r] = (rep, bad_ok, bad_blocks)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rep, bad_ok, bad_blocks = res[0]
+    assert rep["world_size"] == 2 and rep["distinct_devices"] == 2
+    assert rep["gathered_check"] is True and rep["gathered_blocks_ok"] == [True, True]
+    assert [r["rank"] for r in rep["ranks"]] == [0, 1]
+    assert [r["device_index"] for r in rep["ranks"]] == [0, 1]
+    assert [r["elapsed_ms"] for r in rep["ranks"]] == [250.0, 1250.0]
+    assert all(r["kernel_ms"] == 1.5 and r["n_regrets"] == 5 for r in rep["ranks"])
+    assert bad_ok is False and bad_blocks == [True, False]
+
+
 def test_shard_covers_exactly():
     for total in (0, 1, 7, 1000, 1001):
         for world in (1, 2, 3, 8):

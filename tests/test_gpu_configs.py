@@ -37,6 +37,39 @@ def _free_device_memory(eng):
     eng.release_buffers()
 
 
+def test_config0_driver_single_ftl_run(eng):
+    """configs[0] at its stated size: one FTL run, d = 2, T = 1000, one random sequence,
+    through both drop-ins the reference's drivers import (driver.py:204-226 takes
+    ``algorithms``; fast_driver.py:23-28 ``fast_algorithms``, fast_algorithms.py:88-115 and
+    :171-177).  float64: bit-exact vs the oracle.  float32 twin: bit-exact vs the twin's
+    NumPy calls (tests/golden/twin32.npz ``cfg0_*``, made by make_twin32.py) and the
+    oracle's restatement; the two precisions within the twin's ~1e-6 of each other."""
+    import os
+    from online_convex_optimization_amd import algorithms as A
+    from online_convex_optimization_amd import fast_algorithms as FA
+    with np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                              "twin32.npz"), allow_pickle=False) as f:
+        z32, y32, runs, res = f["cfg0_z"], f["cfg0_y"], f["cfg0_runs"], f["cfg0_res"]
+    assert z32.shape[1:] == (1000, 2)
+    for b in range(z32.shape[0]):
+        z, y = z32[b], y32[b]
+        for i, (a, e) in enumerate(runs):
+            a = int(a)
+            r64 = FA.simulate_alg(z, y, a, float(e))        # float32 rows, as driver callers pass
+            want64 = O.simulate_alg(z.astype(np.float64), y.astype(np.float64), a, float(e))
+            assert type(r64) is float and r64 == want64, (b, a, e, r64, want64)
+            r32 = A.simulate_alg(z, y, a, float(e))
+            assert type(r32) is np.float32 and r32 == res[i, b], (b, a, e, r32, res[i, b])
+            assert r32 == O.t32_simulate_alg_full(z, y, a, float(e))[0]
+            assert abs(float(r32) - r64) <= 1e-4 * max(1.0, abs(r64)), (b, a, e, r32, r64)
+    # the g(T) sampler at d = 2 generated on device, FTL, vs the oracle
+    db = eng.DeviceBatch(4, 1000, 2, lanes_per_seq=1).generate_gT(base_seed=0)
+    reg = db.simulate_alg(alg_flag=1).cpu().numpy()
+    for r in range(4):
+        zz, yy = O.gT_sample(0, 1000, r, 2)
+        assert reg[r] == O.simulate_alg(zz, yy, 1, SQ2), r
+
+
 def test_config3_T1e5_resident_batch(eng):
     """configs[3], T = 1e5, d = 64: the sweep's resident batch (4 900 runs, ≈255 GB of
     tiles) on the default path vs exact mode and the oracle; g(T) reduced on device."""

@@ -152,3 +152,26 @@ def test_random_families_T1e4(eng, family, runs, reps):
         z, y, _ = fn(int(seeds[b % B]), T, int(rep_idx[b % B]))
         ref, rsw = O.simulate_SMART_like(z, y, th[b], SQ2, return_switch=True)
         assert close_closed(reg[b], ref, T) and sw[b] == rsw, (family, b, reg[b], ref, sw[b], rsw)
+
+
+def test_non_finite_thresholds_decide_without_rescan(eng):
+    """thresh = +inf (never switch), -inf (switch at step 0), NaN (`>= NaN` is false: never)
+    and a huge finite one: the closed-prefix kernel decides every step without re-scanning
+    the prefix (an infinite threshold used to widen the rounding band to infinity and send
+    every step to the O(t) re-scan), with the reference's switch steps and regrets."""
+    import torch
+    B, T, d = 4, 300, 8
+    th = np.array([np.inf, -np.inf, np.nan, 1e300])
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=1).generate_gT(base_seed=5)
+    sw = torch.full((B,), -7, dtype=torch.int64, device=db.device)
+    st = torch.zeros(2, dtype=torch.int64, device=db.device)
+    reg = db.simulate_smart(th, SQ2, switch_step=sw, closed_prefix=True,
+                            closed_comparator=False, stats=st).clone()
+    torch.cuda.synchronize()
+    reg, sw, st = reg.cpu().numpy(), sw.cpu().numpy(), st.cpu().numpy()
+    assert st[0] == 0, st
+    assert list(sw) == [-1, 0, -1, -1]
+    for b in range(B):
+        z, y = O.gT_sample(5, T, b, d)
+        ref, rsw = O.simulate_SMART_like(z, y, float(th[b]), SQ2, return_switch=True)
+        assert reg[b] == ref and sw[b] == rsw, (b, reg[b], ref, sw[b], rsw)
