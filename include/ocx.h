@@ -47,11 +47,12 @@
 #define OCX_H_
 
 #define OCX_LANES_BEST 128
-/* ocx_version() == OCX_VERSION = 10000 * major + 100 * minor + patch (300 = 0.3.0).  0.2.0:
+/* ocx_version() == OCX_VERSION = 10000 * major + 100 * minor + patch (400 = 0.4.0).  0.2.0:
  * ocx_ftrl_vs_exact_batch has its round-1 signature again (the `norm` argument moved to
  * ocx_ftrl_vs_exact_batch_ex); callers built against 0.1.x check ocx_version() >= 200.
  * 0.3.0 adds the general exact-FTL solver (ocx_exact_ball_solve, ocx_dev_exact_ball_solve,
- * ocx_dev_exact_ball_solve_tiled); nothing existing changed.
+ * ocx_dev_exact_ball_solve_tiled); nothing existing changed.  0.4.0 adds
+ * ocx_dev_gen_simulate (generation overlapped with FTRL); nothing existing changed.
  *
  * Checking the ABI: one intermediate 0.1.x tree exported ocx_ftrl_vs_exact_batch WITH a
  * `norm` argument under the same symbol and the same version number as the release without
@@ -60,7 +61,7 @@
  * compiled with (OCX_ABI_MATCHES() below), not ocx_version() >= some minimum, and must take
  * `norm` through ocx_ftrl_vs_exact_batch_ex only.  The Python binding (_lib.py) checks
  * equality the same way. */
-#define OCX_VERSION 300
+#define OCX_VERSION 400
 
 #include <stddef.h>
 #include <stdint.h>
@@ -400,6 +401,30 @@ int ocx_dev_exact_ball_solve_tiled(const ocx_layout* L, const double* z_tiled,
 /* Max over runs of regrets[B] (device) into *gmax (device), starting from 0.0
  * as fast_algorithms.py:228,242-243 does. */
 int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* stream);
+
+/* fast_algorithms.py:230-247's inner loop over resident batches: for k < nbatch, the runs
+ * run0 + k*B .. run0 + (k+1)*B - 1 are generated on device into z_tiled / y_tiled
+ * (ocx_dev_gen_gT) and simulated by FTRL (alg_flag 0, eta0; the certified closed-form
+ * comparator unless OCX_GENSIM_TWO_PASS, as ocx_gT_regrets does).  regret [B] (device,
+ * required: every batch's regrets pass through it) holds the last batch's regrets; gmax (device double, nullable) receives
+ * max(0, max over every batch's regrets), bit-identical to the host loop.  Queued on
+ * `stream`; complete when the stream reaches this point.
+ *   Pipelined (the default where supported: d = 64 with the 8 x 8 or 16 x 4 butterfly
+ * layout): the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator
+ * round) and sub-batch i+1 is generated while the FTRL kernel reads sub-batch i on a second
+ * stream of the library's, the generator capped at three waves per SIMD and the FTRL kernel
+ * in a 128-VGPR form so both stay resident (csrc/ocx_pipeline.hip); consecutive batches
+ * overlap the same way.  Same kernels and arithmetic as the sequential path: the regrets are
+ * bit-identical to it.
+ *   OCX_GENSIM_SEQUENTIAL: generate, then simulate, batch by batch on `stream` (any layout).
+ *   OCX_GENSIM_TWO_PASS: the reference's streamed comparator pass instead of the certified
+ *     closed form (what the bit-exact layouts ask for; the regrets are then bit-identical to
+ *     fast_algorithms.py in those layouts). */
+#define OCX_GENSIM_SEQUENTIAL 1u
+#define OCX_GENSIM_TWO_PASS 2u
+int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, int64_t nbatch,
+                         double* z_tiled, double* y_tiled, double eta0, double* regret,
+                         double* gmax, uint32_t flags, int64_t sub_seqs, void* stream);
 
 #ifdef __cplusplus
 }

@@ -5,6 +5,6 @@ Drop-in modules (same names/signatures as the reference's):
 Batched / device-resident API: engine
 C ABI: include/ocx.h (libocx.so, built by _build.py)
 """
-__version__ = "0.3.0"
+__version__ = "0.4.0"
 
 from . import _lib  # noqa: F401

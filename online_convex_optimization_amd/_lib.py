@@ -85,6 +85,8 @@ SIGNATURES = {
     "ocx_dev_replay": (c_int, [ctypes.POINTER(Layout), ctypes.POINTER(Layout), c_vp, c_vp, c_vp,
                                c_vp, c_vp, c_vp]),
     "ocx_dev_max_regret": (c_int, [c_vp, c_i64, c_vp, c_vp]),
+    "ocx_dev_gen_simulate": (c_int, [ctypes.POINTER(Layout), c_u64, c_i64, c_i64, c_vp, c_vp,
+                                     c_double, c_vp, c_vp, ctypes.c_uint32, c_i64, c_vp]),
     "ocx_dev_simulate_alg_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_int, c_double, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "ocx_dev_ftrl_vs_exact_ex": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_vp, c_vp,
@@ -111,12 +113,14 @@ TEST_SIGNATURES = {
     "ocx_test_gT_regrets_unclean": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp,
                                             c_int, c_int, c_i64]),
 }
-OCX_VERSION = 300  # include/ocx.h OCX_VERSION: the ABI these signatures describe
+OCX_VERSION = 400  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1
 OCX_EXACT_BALL_MAX_D = 10  # include/ocx.h
 OCX_ALG_CLOSED_COMPARATOR = 2
 OCX_ALG_TREE_SUMS = 4
 OCX_SMART_CLOSED_PREFIX = 8
+OCX_GENSIM_SEQUENTIAL = 1
+OCX_GENSIM_TWO_PASS = 2
 
 _lib = None
 _lock = threading.Lock()

@@ -26,23 +26,30 @@
 // FTL near θ = 0, where ||θ_t||² = U + g(2V + gW) would lose relative accuracy to
 // cancellation, re-sums ||θ_t||² directly (||θ_t||² < 0.25: early steps, returns to the
 // origin).  The comparator pass / closed form are those of ocx_alg_kernel.
+#include <cstdlib>
+
 #include "ocx_device_math.h"
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
-template <int C, int P, int NB, bool FTL>
-__global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
+// MINW: waves per SIMD the register allocation must allow (1: the whole file; 4: at most
+// 128 VGPRs, the lean form the overlapped pipeline runs beside the generator,
+// ocx_pipeline.hip).  The launch covers wave-groups [g0, g0 + gn) of the layout.
+template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1>
+__global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
-    double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass) {
+    double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
+    int64_t gn) {
     static_assert(P >= 2 && NB >= 4, "butterfly layouts, a ring holding z_{t-1} .. z_{t+1}");
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
     // wave-uniform, provably (readfirstlane): the tile bases live in SGPRs and every load
     // is an SGPR base + the lane's constant offset, with no per-load address arithmetic
-    const int64_t g = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_wave_id());
-    if (g >= G) return;
+    const int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_wave_id());
+    if (wv >= gn) return;
+    const int64_t g = g0 + wv;
 #ifdef OCX_ALG_PRIO  // tuning: issue priority over waves of a kernel running beside it
     __builtin_amdgcn_s_setprio(OCX_ALG_PRIO);
 #endif
@@ -82,7 +89,111 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
     };
     double cum = 0.0;
     double scv = 0.0;  // −η0/√(t+1+lane) for the 64 steps from the last multiple of 64
-    ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+
+    // ---- CAND: the step's action for every value g_{t-1} can take, formed a step early.
+    // g is −½, 0 or +½, so z_t·θ_t = A + g·Bz and ||θ_t||² = U + g(2V + gW) have three
+    // possible values; their butterflies, sqrt and division — everything the plain pipelined
+    // step does after g_{t-1} arrives — are formed for g = ±½ at the end of step t−1 (beside
+    // step t−1's own chain), and step t only selects.  The selected values are the ones the
+    // plain step computes from the same lane partials, bit for bit.  g = 0 (an exact tie) is
+    // formed when it happens (a wave-uniform branch on the chain, rare outside the flip /
+    // switching families).
+    double qq_m = 0.0, qq_p = 0.0;  // step t's q_t for g_{t-1} = −½ / +½
+    double zl_m = 0.0, zl_p = 0.0, tl_m = 0.0, tl_p = 0.0;  // their lane partials
+    // q from the lane partials of z_t·θ_t (zl) and ||θ_t||² (tl) at step t1; FTL near the
+    // origin re-sums ||θ_t||² directly from θ_t = th + g·zc (as the plain step does)
+    auto q_of = [&](double zl, double& tl, double g, const ocx_d2* zc, int64_t t1) -> double {
+        const double q_raw = ocx_seq_sum<P>(zl);
+        double n_raw = ocx_seq_sum<P>(tl);
+        if constexpr (!FTL) {
+            const double sc = ocx_readlane(scv, (int)(t1 & 63));
+            const double a = sc * q_raw;
+            const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+            return s_abs > 1.0 ? a * (1.0 / s_abs) : a;
+        } else {
+            if (__ballot(n_raw < 0.25) != 0) {  // wave-uniform; per sequence below
+                double p[C];
+#pragma unroll
+                for (int j = 0; j < C; ++j) {
+                    const double tj = __builtin_fma(g, ocx_zj(zc, j), th[j]);
+                    p[j] = tj * tj;
+                }
+                const double tld = ocx_lane_sum<C>(p);
+                const double nd = ocx_seq_sum<P>(tld);
+                if (n_raw < 0.25) {
+                    tl = tld;
+                    n_raw = nd;
+                }
+            }
+            return n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
+        }
+    };
+    auto make_cand = [&](const ocx_d2* zc, int64_t t1) {
+        const double v2 = 2.0 * V;
+        zl_m = __builtin_fma(-0.5, Bz, A);
+        zl_p = __builtin_fma(0.5, Bz, A);
+        tl_m = __builtin_fma(-0.5, __builtin_fma(-0.5, W, v2), U);
+        tl_p = __builtin_fma(0.5, __builtin_fma(0.5, W, v2), U);
+        qq_m = q_of(zl_m, tl_m, -0.5, zc, t1);
+        qq_p = q_of(zl_p, tl_p, 0.5, zc, t1);
+    };
+    if constexpr (CAND) {
+        if constexpr (!FTL) scv = -(eta0 / sqrt((double)(1 + lane)));
+        make_cand(zb[NB - 1], 0);  // θ_0 = 0 whatever g_{-1}: every candidate is q_0
+    }
+
+    if constexpr (CAND) ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+        const ocx_d2* zp1 = zb[(u + NB - 1) % NB];  // z_{t-1}
+        // ---- chain: g_{t-1} → select q_t → g_t
+        double q = gp > 0.0 ? qq_p : qq_m;
+        double zth = gp > 0.0 ? zl_p : zl_m;
+        double tth = gp > 0.0 ? tl_p : tl_m;
+        if (__ballot(gp == 0.0) != 0) {  // an exact tie last step: θ_t = θ_{t-1}
+            double tl0 = U;
+            const double q0 = q_of(A, tl0, 0.0, zp1, t);
+            if (gp == 0.0) {
+                q = q0;
+                zth = A;
+                tth = tl0;
+            }
+        }
+        const double yv = yb[u];
+        const double diff = q - yv;  // :106-111
+        cum += 0.5 * fabs(diff);
+        const double gq = ocx_grad(diff);
+        clean = clean && fabs(yv) == 1.0 && gq == -0.5 * yv;
+
+        // ---- beside the chain: θ_t, step t+1's lane partials and its candidates
+#pragma unroll
+        for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, ocx_zj(zp1, j), th[j]);
+        const ocx_d2* zc = zb[u];
+        const ocx_d2* zn = zb[(u + 1) % NB];
+        double w = 0.0, an = 0.0, bn = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+            const double zj = ocx_zj(zc, j);
+            w = __builtin_fma(zj, zj, w);
+            an = __builtin_fma(ocx_zj(zn, j), th[j], an);
+            bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
+        }
+        if (onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);
+        V = zth;
+        W = w;
+        A = an;
+        Bz = bn;
+        gp = gq;
+        if (((t + 1) & 63) == 0) {  // as the plain step's refresh at the top of step t+1
+            if constexpr (!FTL) scv = -(eta0 / sqrt((double)(t + 2 + lane)));
+            double uu = 0.0;
+#pragma unroll
+            for (int j = 0; j < C; ++j) uu = __builtin_fma(th[j], th[j], uu);
+            U = uu;
+        } else {
+            U = tth;
+        }
+        make_cand(zc, t + 1);
+    });
+    else ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
         // every 64 steps: the FTRL scales of the next 64 steps (one per lane, one sqrt/div
         // per lane instead of one per step) and ||θ||²'s lane part summed afresh, so the
         // running update below drifts for at most 64 steps
@@ -184,21 +295,42 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_alg_pipe_kernel(
 }
 
 namespace {
-template <int C, int P>
-hipError_t launch_pipe_cp(const ocx_layout* L, const double* zt, const double* yt, int ftl,
-                          double eta0, double* reg, double* cum, double* comp, int* closed_out,
-                          int onepass, hipStream_t st) {
+// CAND (candidate actions formed a step early) where one wave's step latency sets the time:
+// launches of at most OCX_PIPE_CAND_MAX_WAVES waves (2 per SIMD by default).  Beyond that
+// the plain pipelined step streams at the HBM ceiling already and the candidates' extra
+// VALU work (two butterflies, a sqrt and a division per step) buys nothing.
+// OCX_PIPE_CAND=0/1 forces either form (tuning, tests; read at every launch).
+bool pipe_cand(const ocx_layout* L) {
+    // read per launch (a getenv per kernel launch is noise), so one process can A/B both
+    if (const char* e = std::getenv("OCX_PIPE_CAND")) return std::atoi(e) != 0;
+    const char* m = std::getenv("OCX_PIPE_CAND_MAX_WAVES");
+    return L->G <= (m ? (int64_t)std::atoll(m) : (int64_t)2048);
+}
+
+template <int C, int P, bool FTL, bool CAND>
+hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt, double eta0,
+                         double* reg, double* cum, double* comp, int* closed_out, int onepass,
+                         hipStream_t st) {
     // z_{t-1} .. z_{t+1} must be in the ring, and the late loads (ocx_ring_loop) keep NB-2
     // steps in flight: one slot more than the plain kernel's ring
     constexpr int NB = nb_for(C, P) + 1 < 4 ? 4 : nb_for(C, P) + 1;
     const dim3 grid = ocx_grid(L->G, ocx_block_waves(L->G)), block(64 * ocx_block_waves(L->G));
-    if (ftl)
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, true>), grid, block, 0, st, zt, yt, L->B,
-                           L->T, L->G, eta0, reg, cum, comp, closed_out, onepass);
-    else
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false>), grid, block, 0, st, zt, yt, L->B,
-                           L->T, L->G, eta0, reg, cum, comp, closed_out, onepass);
+    hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, CAND>), grid, block, 0, st, zt, yt,
+                       L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass, (int64_t)0,
+                       L->G);
     return hipGetLastError();
+}
+
+template <int C, int P>
+hipError_t launch_pipe_cp(const ocx_layout* L, const double* zt, const double* yt, int ftl,
+                          double eta0, double* reg, double* cum, double* comp, int* closed_out,
+                          int onepass, hipStream_t st) {
+    const bool cand = pipe_cand(L);
+    if (ftl)
+        return cand ? launch_pipe_k<C, P, true, true>(L, zt, yt, eta0, reg, cum, comp, closed_out, onepass, st)
+                    : launch_pipe_k<C, P, true, false>(L, zt, yt, eta0, reg, cum, comp, closed_out, onepass, st);
+    return cand ? launch_pipe_k<C, P, false, true>(L, zt, yt, eta0, reg, cum, comp, closed_out, onepass, st)
+                : launch_pipe_k<C, P, false, false>(L, zt, yt, eta0, reg, cum, comp, closed_out, onepass, st);
 }
 
 template <int C>
@@ -233,4 +365,49 @@ hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const doub
         case 32: return launch_pipe_c<32>(L, zt, yt, ftl, eta0, reg, cum, comp, closed_out, onepass, st);
         default: return hipErrorInvalidValue;
     }
+}
+
+// The lean form over wave-groups [g0, g0 + gn) (ocx_pipeline.hip): at most 128 VGPRs, so one
+// wave fits on a SIMD beside three generator waves; a shorter ring (OCX_PIPE_LEAN_NB8 / _NB4
+// slots at 8 / 4 coordinates per lane) is what makes it fit.  FTRL only, the pipeline's
+// algorithm; 8 x 8 and 16 x 4 layouts.
+#ifndef OCX_PIPE_LEAN_NB8
+#define OCX_PIPE_LEAN_NB8 4
+#endif
+#ifndef OCX_PIPE_LEAN_NB4
+#define OCX_PIPE_LEAN_NB4 8
+#endif
+namespace {
+template <int C, int P>
+hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, double eta0,
+                       double* reg, int onepass, int64_t g0, int64_t gn, int cand,
+                       hipStream_t st) {
+    constexpr int NB = C >= 8 ? OCX_PIPE_LEAN_NB8 : OCX_PIPE_LEAN_NB4;
+    const dim3 grid = ocx_grid(gn, 1), block(64);
+    if (cand)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, true, 4>), grid, block, 0, st, zt,
+                           yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr, (double*)nullptr,
+                           (int*)nullptr, onepass, g0, gn);
+    else
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4>), grid, block, 0, st, zt,
+                           yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr, (double*)nullptr,
+                           (int*)nullptr, onepass, g0, gn);
+    return hipGetLastError();
+}
+}  // namespace
+
+bool ocx_pipe_lean_supported(const ocx_layout* L) {
+    return !L->chain && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
+}
+
+hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
+                                    double eta0, double* reg, int onepass, int64_t g0,
+                                    int64_t gn, int cand, hipStream_t st) {
+    if (gn <= 0) return hipSuccess;
+    if (g0 < 0 || g0 + gn > L->G) return hipErrorInvalidValue;
+    if (L->P == 8 && L->C == 8)
+        return launch_lean<8, 8>(L, zt, yt, eta0, reg, onepass, g0, gn, cand, st);
+    if (L->P == 16 && L->C == 4)
+        return launch_lean<4, 16>(L, zt, yt, eta0, reg, onepass, g0, gn, cand, st);
+    return hipErrorInvalidValue;
 }

@@ -449,6 +449,59 @@ int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* str
     return OCX_OK;
 }
 
+}  // extern "C"
+
+namespace {
+hipError_t fold_max(const double* r, int64_t n, void* acc, hipStream_t st) {
+    return launch_max_fold(r, n, static_cast<unsigned long long*>(acc), st);
+}
+
+// ocx_pipeline.hip's knobs (tuning; the defaults are the measured best): generator waves per
+// SIMD beside the FTRL kernel, and the FTRL step form (candidate-select or plain)
+int pipe_wps() {
+    const char* e = std::getenv("OCX_PIPE_WPS");
+    const int v = e ? std::atoi(e) : 3;
+    return v >= 1 && v <= 8 ? v : 3;
+}
+int pipe_cand_default() {
+    const char* e = std::getenv("OCX_PIPE_CAND");
+    return e ? (std::atoi(e) != 0) : 1;
+}
+}  // namespace
+
+extern "C" {
+
+int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, int64_t nbatch,
+                         double* z_tiled, double* y_tiled, double eta0, double* regret,
+                         double* gmax, uint32_t flags, int64_t sub_seqs, void* stream) {
+    if (int rc = check_layout(L)) return rc;
+    if (run0 < 0 || nbatch < 0) return fail(OCX_E_INVALID, "negative run0 / nbatch");
+    if (flags & ~(OCX_GENSIM_SEQUENTIAL | OCX_GENSIM_TWO_PASS))
+        return fail(OCX_E_INVALID, "unknown flags");
+    if (L->B > 0 && !regret) return fail(OCX_E_INVALID, "NULL regret");
+    if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
+    const hipStream_t st = (hipStream_t)stream;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(gmax);
+    if (acc) OCX_HIP(hipMemsetAsync(acc, 0, 8, st));  // +0.0
+    if (nbatch == 0 || L->B == 0 || L->T == 0) return OCX_OK;
+    // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
+    // the reference's streamed pass (the bit-exact modes)
+    const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
+    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L)) {
+        OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
+                                          regret, onepass, acc ? fold_max : nullptr, acc,
+                                          pipe_wps(), sub_seqs, pipe_cand_default(), st));
+        return OCX_OK;
+    }
+    for (int64_t k = 0; k < nbatch; ++k) {
+        OCX_HIP(ocx_launch_gen_gT(L, base_seed, run0 + k * L->B, z_tiled, y_tiled, st));
+        OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, 0, eta0, nullptr, regret, nullptr, nullptr,
+                               nullptr, st, nullptr, nullptr, onepass));
+        if (acc) OCX_HIP(launch_max_fold(regret, L->B, acc, st));
+    }
+    return OCX_OK;
+}
+
 // ---------------------------------------------------------------- host API
 int ocx_simulate_alg_batch(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                            int alg_flag, double eta0, const double* comparator, double* regret,

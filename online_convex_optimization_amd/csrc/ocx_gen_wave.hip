@@ -817,8 +817,11 @@ __device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, 
 #ifndef OCX_GEN_NW64
 #define OCX_GEN_NW64 8
 #endif
-__host__ __device__ constexpr int gen_block(int DF, bool LR) {
-    return 64 * ((DF == 64 && !LR) ? OCX_GEN_NW64 : 4);
+// OV (the overlapped pipeline, ocx_pipeline.hip): four-wave blocks of the default d = 64
+// form, so the launcher can cap the generator at three blocks (waves) per CU (SIMD) through
+// its LDS request and leave each SIMD room for one FTRL wave beside it.
+__host__ __device__ constexpr int gen_block(int DF, bool LR, bool OV = false) {
+    return 64 * ((DF == 64 && !LR && !OV) ? OCX_GEN_NW64 : 4);
 }
 #ifdef OCX_GEN_TUNE_NO_STORE  // tuning only: rows computed, not written
 #define OCX_GEN_STORE(v, p) do { if ((v) == 1234.5) *(p) = (v); } while (0)
@@ -871,14 +874,16 @@ constexpr int kRows64 = 8;
 // (a register budget of 80 VGPRs, a few cold spills) where the default form keeps four.
 // RAW (DF = 0 only): rows left unclipped, for the float32 twin (ocx_twin32.hip), which
 // rounds them to float and clips them in float32 itself (algorithms.py:157-160).
-template <int MODE, int DF, bool LR = false, bool RAW = false>
-__global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
+// b_off: the launch covers sequences [b_off, b_off + nseq) of the layout (a sub-batch of the
+// overlapped pipeline; 0 otherwise), a multiple of the block's waves.
+template <int MODE, int DF, bool LR = false, bool RAW = false, bool OV = false>
+__global__ __launch_bounds__(gen_block(DF, LR, OV), OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
     const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out, int rb,
-    int64_t nwaves) {
-    constexpr int kBlock = gen_block(DF, LR);
+    int64_t nwaves, int64_t b_off) {
+    constexpr int kBlock = gen_block(DF, LR, OV);
     constexpr int kNW = kBlock / 64;
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
     constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && (DF == 64 || (DF == 1024 && OCX_GEN_1K_FLAT));
@@ -955,7 +960,7 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
     // mode's buffered half-draw makes rounds differ per sequence; nseq and nwaves multiples of
     // kNW, checked here and arranged by the launcher).
     const bool stage_y = OCX_GEN_STAGE_Y && MODE == 0 && lab_in == nullptr &&
-                         nwaves % kNW == 0 && nseq % kNW == 0;
+                         nwaves % kNW == 0 && nseq % kNW == 0 && b_off % kNW == 0;
     // b0: the block's first sequence of this pass (the block's waves hold b0 .. b0 + kNW - 1)
     auto store_y_round = [&](int64_t tl, int64_t b0) {
         __syncthreads();  // every wave's round is in its ring
@@ -974,7 +979,7 @@ __global__ __launch_bounds__(gen_block(DF, LR), OCX_GENW_MIN_WAVES_FOR(DF, LR)) 
         }
         __syncthreads();  // the rings are free again
     };
-    for (int64_t b = wave; b < nseq; b += nwaves) {
+    for (int64_t b = b_off + wave; b < b_off + nseq; b += nwaves) {
         const int64_t g = b / S;
         const int s = (int)(b - g * S);
         double* yrow = ytl + g * T * S + s;
@@ -1377,9 +1382,74 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     const int64_t nwaves = (int64_t)blocks * (kBlock / 64);
     hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR, RAW>), dim3(blocks), dim3(kBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
-                       st_out, lab_in, lab_out, rb, nwaves);
+                       st_out, lab_in, lab_out, rb, nwaves, (int64_t)0);
     return hipGetLastError();
 }
+
+// The overlapped pipeline's generator (ocx_pipeline.hip): the d = 64 default form in four-wave
+// blocks over sequences [b_off, b_off + nseq) of L, at most `wps` waves per SIMD.  The cap is
+// set through the LDS request (each block asks for a CU's LDS / wps, so no CU takes more than
+// wps blocks) and leaves every SIMD the registers of one more wave for the FTRL kernel running
+// beside it on another stream.  One wave per stream (nseq <= the cap's resident waves makes a
+// single round).
+struct OvGeom {
+    size_t lds = 0;
+    int per_cu = 0;
+};
+OvGeom ov_geometry(int dev, int wps) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, OvGeom> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, wps);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    OvGeom gm;
+    int lds_cu = 0;
+    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) !=
+            hipSuccess || lds_cu <= 0)
+        lds_cu = 160 * 1024;
+    const size_t base = (size_t)ring_doubles(64, 64) * 8 * 4;  // four waves' rings
+    size_t lds = base;
+    int q = 0;
+    for (; lds <= (size_t)lds_cu; lds += 512) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, 64, false, false, true>,
+                                                         256, lds) != hipSuccess)
+            break;
+        if (q <= wps) break;
+    }
+    gm.lds = lds;
+    gm.per_cu = q;
+    cache.emplace(key, gm);
+    return gm;
+}
+
+}  // namespace
+
+hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                   int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
+                                   hipStream_t st) {
+    if (nseq <= 0 || L->T == 0) return hipSuccess;
+    if (L->d != 64 || L->P * L->C != 64 || b_off % 4 || nseq % 4) return hipErrorInvalidValue;
+    if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    const OvGeom gm = ov_geometry(dev, wps);
+    const int64_t resident = (int64_t)cus * 4 * std::max(1, std::min(gm.per_cu, wps));
+    const int64_t per_wave = (nseq + resident - 1) / resident;
+    const unsigned blocks = (unsigned)(((nseq + per_wave - 1) / per_wave + 3) / 4);
+    const int64_t nwaves = (int64_t)blocks * 4;
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, true>), dim3(blocks), dim3(256),
+                       gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d, (int)L->P,
+                       (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                       (const uint64_t*)nullptr, (uint64_t*)nullptr, ring_doubles(64, 64), nwaves,
+                       b_off);
+    return hipGetLastError();
+}
+
+namespace {
 
 template <int MODE>
 hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq,

@@ -1,0 +1,127 @@
+// ocx_pipeline.hip — generation of the g(T) adversary overlapped with the FTRL pass
+// (fast_algorithms.py:230-247: each run's z, y drawn, then simulated).
+//
+// The two kernels are bound by different units: the generator (ocx_gen_wave.hip) by the
+// VALU — a 128-bit LCG and the ziggurat per normal, ≈74 VALU + 39 SALU instructions per
+// 64-normal row, writing at ≈3 TB/s — and the FTRL kernel by HBM reads (one pass, 6.3–6.5
+// TB/s).  Run one after the other they take gen + FTRL (57.4 + 26.1 ms per 32 768 × 1e4 × 64
+// batch).  Here a resident batch is cut into sub-batches of sequences; sub-batch i+1 is
+// generated while the FTRL kernel reads sub-batch i on a second stream.  Two things make
+// the kernels share the CUs instead of queueing behind each other:
+//   * the generator runs in four-wave blocks whose LDS request admits at most `wps` (3)
+//     blocks per CU, i.e. 3 of its 128-VGPR waves per SIMD (ocx_launch_gen_gT_range);
+//   * the FTRL kernel runs in its lean form (<= 128 VGPRs, ocx_launch_alg_pipe_lean), so one
+//     FTRL wave fits on every SIMD beside them whenever its sub-batch is ready.
+// A sub-batch is one round of generator waves (one stream per wave), so no generator wave
+// idles at a sub-batch's end.  Sub-batch i of batch k+1 is generated into the region FTRL
+// read for sub-batch i of batch k, after that read (events), so consecutive batches overlap
+// too.  The kernels, and so every regret, are the sequential path's, bit for bit.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+#include <vector>
+
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+struct PipeCtx {
+    std::mutex mu;
+    bool init = false;
+    hipStream_t sim = nullptr;
+    std::vector<hipEvent_t> ev_gen, ev_sim;
+    std::vector<char> sim_recorded;
+};
+PipeCtx g_pipe[64];
+
+hipError_t ensure_events(PipeCtx& c, size_t n) {
+    while (c.ev_gen.size() < n) {
+        hipEvent_t a, b;
+        hipError_t e = hipEventCreateWithFlags(&a, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        e = hipEventCreateWithFlags(&b, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        c.ev_gen.push_back(a);
+        c.ev_sim.push_back(b);
+        c.sim_recorded.push_back(0);
+    }
+    return hipSuccess;
+}
+
+int64_t lcm64(int64_t a, int64_t b) {
+    int64_t x = a, y = b;
+    while (y) {
+        const int64_t t = x % y;
+        x = y;
+        y = t;
+    }
+    return a / x * b;
+}
+
+#define OCX_PIPE_TRY(expr)                    \
+    do {                                      \
+        hipError_t e_ = (expr);               \
+        if (e_ != hipSuccess) return e_;      \
+    } while (0)
+
+}  // namespace
+
+bool ocx_pipeline_supported(const ocx_layout* L) {
+    return L->d == 64 && L->P * L->C == 64 && ocx_pipe_lean_supported(L) && L->T > 0 &&
+           L->T * L->d < ((int64_t)1 << 32);
+}
+
+// nbatch batches of L->B runs each (runs run0 + k·B, k < nbatch) through one z/y buffer of
+// layout L; regret[] holds the last batch's regrets, dmax (nullable, device) folds the max
+// over all of them (ocx_max_fold: bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
+// one generator round per sub-batch.  Returns with the work queued on `st` (joined).
+hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                     int64_t nbatch, double* zt, double* yt, double eta0,
+                                     double* regret, int onepass,
+                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
+                                     void* fold_arg, int wps, int64_t sub_seqs, int cand,
+                                     hipStream_t st) {
+    if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    OCX_PIPE_TRY(hipGetDevice(&dev));
+    OCX_PIPE_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    PipeCtx& c = g_pipe[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (!c.init) {
+        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.sim, hipStreamNonBlocking));
+        c.init = true;
+    }
+    const int64_t S = L->S;
+    const int64_t Bp = L->G * S;  // sequences of the layout, padding included
+    // sub-batch: whole wave-groups and whole four-wave generator blocks
+    const int64_t unit = lcm64(S, 4);
+    int64_t sub = sub_seqs > 0 ? sub_seqs : (int64_t)cus * 4 * std::max(1, wps);
+    sub = std::max(unit, (sub + unit - 1) / unit * unit);
+    const int64_t nsub = (Bp + sub - 1) / sub;
+    OCX_PIPE_TRY(ensure_events(c, (size_t)nsub));
+    std::fill(c.sim_recorded.begin(), c.sim_recorded.end(), 0);
+    for (int64_t k = 0; k < nbatch; ++k) {
+        const int64_t r0 = run0 + k * L->B;
+        for (int64_t i = 0; i < nsub; ++i) {
+            const int64_t b0 = i * sub, nb = std::min(sub, Bp - b0);
+            // this region's previous reader (sub-batch i of batch k-1) must be done
+            if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)i], 0));
+            OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st));
+            OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], st));
+            OCX_PIPE_TRY(hipStreamWaitEvent(c.sim, c.ev_gen[(size_t)i], 0));
+            OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
+                                                  cand, c.sim));
+            const int64_t nreal = std::min(nb, L->B - b0);
+            if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, c.sim));
+            OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], c.sim));
+            c.sim_recorded[(size_t)i] = 1;
+        }
+    }
+    // the caller's stream sees every FTRL pass and fold done (the sim stream runs in order)
+    if (nsub > 0 && nbatch > 0) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)nsub - 1], 0));
+    return hipSuccess;
+}

@@ -19,6 +19,26 @@ bool ocx_pipe_supported(const ocx_layout* L);
 hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const double* yt, int ftl,
                                double eta0, double* reg, double* cum, double* comp,
                                int* closed_out, int onepass, hipStream_t st);
+// the lean form over wave-groups [g0, g0 + gn) (<= 128 VGPRs; FTRL, 8 x 8 and 16 x 4 layouts),
+// the FTRL side of the overlapped pipeline (ocx_pipeline.hip); cand: candidate-select step
+bool ocx_pipe_lean_supported(const ocx_layout* L);
+hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
+                                    double eta0, double* reg, int onepass, int64_t g0,
+                                    int64_t gn, int cand, hipStream_t st);
+// g(T) sampler over sequences [b_off, b_off + nseq) of a d = 64 layout, at most wps waves per
+// SIMD (four-wave blocks; ocx_gen_wave.hip)
+hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                   int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
+                                   hipStream_t st);
+// generation overlapped with FTRL (ocx_pipeline.hip): nbatch batches of L->B runs from run0,
+// regret = the last batch's, fold(regret_sub, n, fold_arg, stream) after every sub-batch
+bool ocx_pipeline_supported(const ocx_layout* L);
+hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                     int64_t nbatch, double* zt, double* yt, double eta0,
+                                     double* regret, int onepass,
+                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
+                                     void* fold_arg, int wps, int64_t sub_seqs, int cand,
+                                     hipStream_t st);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

@@ -639,6 +639,27 @@ class DeviceBatch:
             self.comp[:B] = torch.where(ok, self.comp[:B], gcomp)
         return regime
 
+    def generate_simulate(self, base_seed: int = 0, run0: int = 0, nbatch: int = 1,
+                          eta0: float = SQRT2, gmax=None, pipelined: bool = True,
+                          sub_seqs: int = 0):
+        """fast_algorithms.py:230-247's loop over ``nbatch`` resident batches in one call
+        (ocx_dev_gen_simulate): batch k holds runs run0 + k*B .. run0 + (k+1)*B - 1,
+        generated on device into this batch's z/y and simulated by FTRL.  self.regret gets
+        the last batch's regrets; ``gmax`` ([1] float64 device tensor, optional) the max over
+        every batch, from 0.0.  ``pipelined`` overlaps generation of one sub-batch with the
+        FTRL pass over the previous one (d = 64, 8 x 8 / 16 x 4 butterfly layouts; otherwise,
+        or with False, batch by batch).  The closed-form comparator is taken as in
+        simulate_alg (the bit-exact layouts keep the streamed pass).  Same regrets either way,
+        bit for bit."""
+        flags = 0 if pipelined else _lib.OCX_GENSIM_SEQUENTIAL
+        if self.exact:
+            flags |= _lib.OCX_GENSIM_TWO_PASS
+        _lib.call("ocx_dev_gen_simulate", self._lp(), int(base_seed), int(run0), int(nbatch),
+                  self.z.data_ptr(), self.y.data_ptr(), float(eta0), self.regret.data_ptr(),
+                  gmax.data_ptr() if gmax is not None else None, flags, int(sub_seqs), self._sp)
+        self.rows_clipped = True
+        return self.regret
+
     def max_regret(self, out=None):
         torch = self.torch
         if out is None:

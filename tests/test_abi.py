@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(header, table):
 def test_version_and_error_channel():
     with open(os.path.join(ROOT, "include", "ocx.h")) as f:
         ver = int(re.search(r"#define OCX_VERSION (\d+)", f.read()).group(1))
-    assert _lib.load().ocx_version() == ver == _lib.OCX_VERSION == 300
+    assert _lib.load().ocx_version() == ver == _lib.OCX_VERSION == 400
     with pytest.raises(ValueError):
         _lib.layout(-1, 10, 5)
     assert "negative" in _lib.last_error()

@@ -1,0 +1,65 @@
+"""GPU: generation overlapped with FTRL (ocx_dev_gen_simulate, csrc/ocx_pipeline.hip).
+
+The pipelined path runs the same generator and FTRL arithmetic as the sequential
+generate-then-simulate loop (fast_algorithms.py:230-247 over resident batches), split into
+sub-batches on two streams: its regrets and g(T) must be bit-identical to that loop's, and
+the sampled sequences within the closed-form bar of the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.test_gpu_parity import close_closed
+
+pytestmark = pytest.mark.gpu
+SQ2 = math.sqrt(2)
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from online_convex_optimization_amd import _lib, engine
+    assert _lib.device_count() >= 1
+    return engine
+
+
+@pytest.mark.parametrize("B,T,lanes,sub", [(3000, 300, 8, 512), (2048, 257, 16, 0),
+                                           (1000, 64, 128, 0)])
+def test_pipelined_equals_sequential(eng, B, T, lanes, sub):
+    import torch
+    d, nb = 64, 3
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=lanes)
+    out = {}
+    for mode in (False, True):
+        g = torch.zeros(1, dtype=torch.float64, device=db.device)
+        db.regret.zero_()
+        db.generate_simulate(base_seed=9, run0=5, nbatch=nb, gmax=g, pipelined=mode,
+                             sub_seqs=sub)
+        torch.cuda.synchronize()
+        out[mode] = (db.regret[:B].cpu().numpy().copy(), float(g.item()))
+    assert np.array_equal(out[True][0], out[False][0])
+    assert out[True][1] == out[False][1]
+    # the last batch's regrets are those of runs 5 + 2B ..; g(T) over all 3 batches
+    allr = eng.gT_regrets(T, nb * B, base_seed=9, d=d, run0=5, lanes_per_seq=lanes)
+    assert close_closed(out[True][0], allr[2 * B:], T)
+    assert out[True][1] == eng.max_regret(allr) or close_closed(out[True][1], eng.max_regret(allr), T)
+    for b in (0, B - 1):
+        z, y = O.gT_sample(9, T, 5 + 2 * B + b, d)
+        assert close_closed(out[True][0][b], O.simulate_alg(z, y, 0, SQ2), T), b
+
+
+def test_pipelined_exact_layout_two_pass(eng):
+    """A bit-exact layout is not pipelined (sequential fallback) and keeps the reference's
+    streamed comparator: bit-identical to the oracle."""
+    import torch
+    B, T, d = 70, 120, 64
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=1)
+    g = torch.zeros(1, dtype=torch.float64, device=db.device)
+    db.generate_simulate(base_seed=2, run0=0, nbatch=2, gmax=g)
+    torch.cuda.synchronize()
+    reg = db.regret[:B].cpu().numpy()
+    for b in (0, 33, B - 1):
+        z, y = O.gT_sample(2, T, B + b, d)
+        assert reg[b] == O.simulate_alg(z, y, 0, SQ2), b
+    ref = max(0.0, max(O.simulate_alg(*O.gT_sample(2, T, r, d), 0, SQ2) for r in range(2 * B)))
+    assert float(g.item()) == ref

@@ -1,0 +1,59 @@
+"""Round 4: generation overlapped with FTRL (ocx_dev_gen_simulate, csrc/ocx_pipeline.hip)
+against the sequential gen-then-FTRL loop, on the bench's resident batch (32 768 x 1e4 x 64,
+OCX_LANES_BEST).  One JSON line per configuration: ms per batch, timesteps/s, fraction of
+2*(8d+8) B/step, and whether the regrets and g(T) are bit-identical to the sequential path.
+Knobs per line: OCX_PIPE_WPS (generator waves per SIMD), OCX_PIPE_CAND (FTRL step form),
+sub_seqs (sequences per sub-batch; 0 = one generator round)."""
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from online_convex_optimization_amd import engine  # noqa: E402
+
+
+def run(db, nb, pipelined, sub=0):
+    g = torch.zeros(1, dtype=torch.float64, device=db.device)
+    db.generate_simulate(0, 0, 1, gmax=g, pipelined=pipelined, sub_seqs=sub)  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    db.generate_simulate(0, 0, nb, gmax=g, pipelined=pipelined, sub_seqs=sub)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return dt / nb * 1e3, db.regret[:db.L.B].cpu().numpy().copy(), float(g.item())
+
+
+def main():
+    B = int(os.environ.get("OCX_PROBE_B", 32768))
+    T = int(os.environ.get("OCX_PROBE_T", 10000))
+    d = 64
+    nb = int(os.environ.get("OCX_PROBE_NB", 4))
+    db = engine.DeviceBatch(B, T, d)
+    ms0, r0, g0 = run(db, nb, False)
+    rate = lambda ms: B * T / (ms * 1e-3)
+    print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
+                      "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
+                      "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0}), flush=True)
+    configs = [("3", "1", 0), ("3", "0", 0), ("2", "1", 0), ("3", "1", 2 * 3 * 1024),
+               ("4", "1", 0)]
+    if os.environ.get("OCX_PROBE_CONFIGS"):
+        configs = [tuple(c.split(":")[:2]) + (int(c.split(":")[2]),)
+                   for c in os.environ["OCX_PROBE_CONFIGS"].split(",")]
+    for wps, cand, sub in configs:
+        os.environ["OCX_PIPE_WPS"] = wps
+        os.environ["OCX_PIPE_CAND"] = cand
+        ms, r, g = run(db, nb, True, sub)
+        print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "pipelined",
+                          "wps": int(wps), "cand": cand == "1", "sub_seqs": sub,
+                          "ms_per_batch": ms, "timesteps_per_s": rate(ms),
+                          "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g,
+                          "bitidentical": bool(np.array_equal(r, r0)) and g == g0}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
