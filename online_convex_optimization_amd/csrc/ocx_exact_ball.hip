@@ -171,7 +171,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_exact_ball_kernel(
     }
     double mu = kMu0;
     int it = 0, kend = 0;
-    bool conv = n == 0;  // the empty prefix: x = 0, as compute_prefix_actions (:296-298) sets it
+    bool conv = n == 0, broke = false;  // the empty prefix: x = 0, as compute_prefix_actions (:296-298) sets it
     while (!conv && it < kMaxIter) {
         ++it;
         double G[D], H[NH];
@@ -290,8 +290,9 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_exact_ball_kernel(
             // μ has outrun fp64: with the optimal face's directions pinned only by the
             // O(1) ball barrier and the active rows' curvature ~1/μ², the floored Cholesky
             // returns garbage (λ ~1e19).  The iterate is the last centre, accurate to that
-            // μ (the certificate below says how well): stop there.
-            conv = true;
+            // μ (the certificate below says how well): stop there, marked as such
+            // (OCX_EXACT_INFO_BREAKDOWN) — not a converged solve.
+            broke = true;
             break;
         }
         double step = lam > 0.25 ? 1.0 / (1.0 + lam) : 1.0;
@@ -375,7 +376,8 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_exact_ball_kernel(
         for (int j = 0; j < D; ++j) xo[j] = x[j];
         if (obj_out) obj_out[b * NP + slot] = P;
         if (gap_out) gap_out[b * NP + slot] = fmax(P - bound, 0.0);
-        if (info_out) info_out[b * NP + slot] = conv ? it : -it;
+        if (info_out)
+            info_out[b * NP + slot] = broke ? (OCX_EXACT_INFO_BREAKDOWN | it) : (conv ? it : -it);
         if (step_loss) {
             // FTL's loss at step n with this action (replay_exact_ftl, exact_ftl.py:318-323:
             // _dot's sequential sum, then the normalized hinge); 0 for the full prefix

@@ -144,18 +144,44 @@ def exact_ball_solve(z, y, *, norm: str = "l2", all_prefixes: bool = True, devic
     return out
 
 
+EXACT_GAP_RTOL = 1e-6  # a general solve is accepted iff info > 0 and gap <= this * (1 + |obj|)
+
+
+def check_certificates(obj, gap, info, what: str = "exact FTL") -> float:
+    """The general solver's answers are only as good as their certificates
+    (include/ocx.h, ocx_exact_ball_solve): every solve must have finished (info > 0: not
+    ended by the step cap) and certify obj − optimum <= gap <= EXACT_GAP_RTOL·(1 + |obj|).
+    A breakdown stop (OCX_EXACT_INFO_BREAKDOWN) passes only on its certificate.  Raises
+    RuntimeError otherwise — what exact_ftl.py:125-126 does when cvxpy's solve fails — and
+    returns the worst gap."""
+    obj = np.asarray(obj, dtype=np.float64)
+    gap = np.asarray(gap, dtype=np.float64)
+    info = np.asarray(info)
+    if obj.size == 0:
+        return 0.0
+    bad = ~((info > 0) & (gap <= EXACT_GAP_RTOL * (1.0 + np.abs(obj))))
+    if bad.any():
+        k = int(np.flatnonzero(bad.ravel())[0])
+        raise RuntimeError(f"{what}: the general solver did not certify {int(bad.sum())} of "
+                           f"{bad.size} problems (first: info {int(info.ravel()[k])}, gap "
+                           f"{float(gap.ravel()[k]):.3g}, obj {float(obj.ravel()[k]):.6g})")
+    return float(gap.max())
+
+
 def _general_fill(z, y, ok: np.ndarray, norm: str, device: int):
     """Sequences outside the closed form's regime, solved by the general solver: (their
     indices, exact_ball_solve over all prefixes, exact FTL's cumulative loss Σ_n step_loss in
-    step order, the comparator loss obj[:, T]); None when every sequence is in the regime."""
+    step order, the comparator loss obj[:, T], the worst certified gap); None when every
+    sequence is in the regime.  Raises RuntimeError where a solve is not certified."""
     bad = np.flatnonzero(~ok)
     if bad.size == 0:
         return None
     T = z.shape[1]
     res = exact_ball_solve(z[bad], y[bad], norm=norm, all_prefixes=True, device=device)
+    worst = check_certificates(res["obj"], res["gap"], res["info"])
     sl = res["step_loss"][:, :T]
     cum = np.cumsum(sl, axis=1)[:, -1] if T > 0 else np.zeros(bad.size)  # sequential order
-    return bad, res, cum, res["obj"][:, T]
+    return bad, res, cum, res["obj"][:, T], worst
 
 
 def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, device: int = 0,
@@ -184,7 +210,7 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, 
     if check_regime:
         g = _general_fill(z, y, ok, norm, device)
         if g is not None:
-            bad, res, gcum, gcomp = g
+            bad, res, gcum, gcomp, _ = g
             cum[bad], comp[bad], act[bad] = gcum, gcomp, res["actions"][:, T]
     return cum, comp, act, ok
 
@@ -236,13 +262,14 @@ def ftrl_vs_exact_batch(z, y, eta0: float = SQRT2, *, norm: str = "l2",
               rg.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _norm_code(norm),
               int(lanes_per_seq), int(device))
     ok = rg.astype(bool)
+    worst = 0.0
     if check_regime:
         g = _general_fill(z, y, ok, norm, device)
         if g is not None:
-            bad, res, gcum, gcomp = g
+            bad, res, gcum, gcomp, worst = g
             ce[bad], cmp_e[bad], act[bad] = gcum, gcomp, res["actions"][:, T]
     out = {"ftrl": cr - cmp_e, "exact": ce - cmp_e, "cum_ftrl": cr, "cum_exact": ce,
-           "comp": cmp_e, "action": act, "in_regime": ok}
+           "comp": cmp_e, "action": act, "in_regime": ok, "exact_gap_max": worst}
     if with_ftl_comparator:
         out["comp_ftl"] = cmp_f
     return out
@@ -627,17 +654,45 @@ class DeviceBatch:
         regime flags.  Synchronises once (to see whether any sequence left the regime)."""
         torch = self.torch
         regime = self.ftrl_vs_exact(eta0, norm=norm)
-        B, T = self.L.B, self.L.T
+        B, T, d = self.L.B, self.L.T, self.L.d
+        self.exact_gap_max = 0.0
         with self._on_stream():
             ok = regime[:B].bool()
             if bool(ok.all().item()):
                 return regime
-            g = self.exact_general(norm)
-            gcum = g["step_loss"][:B, :T].sum(dim=1)
-            gcomp = g["obj"][:B, T]
-            self.cum_exact[:B] = torch.where(ok, self.cum_exact[:B], gcum)
-            self.comp[:B] = torch.where(ok, self.comp[:B], gcomp)
+            # only the sequences outside the regime: their rows out of the tile, row-major
+            bad = torch.nonzero(~ok).flatten()
+            zb, yb = self.rows_of(bad)
+            nb = int(bad.numel())
+            res = {"actions": torch.zeros((nb, T + 1, d), dtype=torch.float64, device=self.device)}
+            for k in ("obj", "gap", "step_loss"):
+                res[k] = torch.zeros((nb, T + 1), dtype=torch.float64, device=self.device)
+            res["info"] = torch.zeros((nb, T + 1), dtype=torch.int32, device=self.device)
+            _lib.call("ocx_dev_exact_ball_solve", zb.data_ptr(), yb.data_ptr(), nb, T, d,
+                      _norm_code(norm), 1, res["actions"].data_ptr(), res["obj"].data_ptr(),
+                      res["gap"].data_ptr(), res["step_loss"].data_ptr(),
+                      res["info"].data_ptr(), self._sp)
+            self._hold(zb, yb)
+            host = {k: res[k].cpu().numpy() for k in ("obj", "gap", "info", "step_loss")}
+            self.exact_gap_max = check_certificates(host["obj"], host["gap"], host["info"])
+            # exact FTL's cumulative loss in step order (the host path's and the replay's)
+            gcum = np.cumsum(host["step_loss"][:, :T], axis=1)[:, -1] if T > 0 else np.zeros(nb)
+            self.cum_exact[bad] = torch.as_tensor(gcum).to(self.device)
+            self.comp[bad] = res["obj"][:, T]
         return regime
+
+    def rows_of(self, seqs):
+        """z [n, T, d] and y [n, T] (device, row-major, contiguous) of the sequences ``seqs``
+        (device int64 tensor of batch indices), gathered out of the tiled layout
+        (include/ocx.h ocx_layout: z_tiled[((k*G + g)*T + t)*128 + L*2 + e])."""
+        L = self.L
+        K, G, T, S, P = L.C // 2, L.G, L.T, L.S, L.P
+        g, s = seqs // S, seqs % S
+        z5 = self.z[:K * G * T * 128].view(K, G, T, S, P, 2)
+        zs = z5[:, g, :, s, :, :]                      # [n, K, T, P, 2]
+        zs = zs.permute(0, 2, 3, 1, 4).reshape(seqs.numel(), T, P * L.C)[:, :, :L.d]
+        ys = self.y[:G * T * S].view(G, T, S)[g, :, s]  # [n, T]
+        return zs.contiguous(), ys.contiguous()
 
     def generate_simulate(self, base_seed: int = 0, run0: int = 0, nbatch: int = 1,
                           eta0: float = SQRT2, gmax=None, pipelined: bool = True,
