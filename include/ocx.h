@@ -206,7 +206,7 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy: unpinned (validated
  * against scipy's HiGHS LPs and by the certificate). */
 #define OCX_EXACT_INFO_BREAKDOWN (1 << 20)
-#define OCX_EXACT_BALL_MAX_D 10
+#define OCX_EXACT_BALL_MAX_D 64
 int ocx_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                          int norm, int all_prefixes, double* actions, double* obj, double* gap,
                          double* step_loss, int32_t* info, int device);

@@ -427,7 +427,11 @@ hipError_t launch(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_pref
         OCX_EB_CASE(1) OCX_EB_CASE(2) OCX_EB_CASE(3) OCX_EB_CASE(4) OCX_EB_CASE(5)
         OCX_EB_CASE(6) OCX_EB_CASE(7) OCX_EB_CASE(8) OCX_EB_CASE(9) OCX_EB_CASE(10)
 #undef OCX_EB_CASE
-        default: return hipErrorInvalidValue;
+        default:
+            // 10 < d <= 64: the system in LDS, one coordinate per lane (ocx_exact_wide.hip)
+            return ocx_launch_exact_wide(rs.z, rs.y, B, rs.T, d, rs.tiled, rs.P, rs.C, rs.S, rs.G,
+                                         norm, all_prefixes, actions, obj, gap, step_loss, info,
+                                         st);
     }
 }
 

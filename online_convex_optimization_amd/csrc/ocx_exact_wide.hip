@@ -1,0 +1,379 @@
+// ocx_exact_wide.hip — the general exact-FTL comparator (ExactFTLNoClip, exact_ftl.py:83-105,
+// solved by cvxpy at :119-128) for 10 < d <= 64: the same primal log-barrier path as
+// ocx_exact_ball.hip (same barrier, schedule, damping, certificate; see that file), laid out
+// for a d × d Newton system that no longer fits one lane's registers.
+//
+// One wavefront per problem (sequence b, prefix n), DP = 16 / 32 / 64 padded coordinates:
+//   * coordinate vectors (x, u, the gradient, the step) live one coordinate per lane;
+//   * the Hessian Σ_i h_i a_i a_iᵀ is accumulated as an 8 × 8 grid of (DP/8)² blocks, lane
+//     8·bj + bk owning rows bj·DP/8.., columns bk·DP/8.. — (DP/8)² fp64 FMAs per row and lane;
+//   * rows are staged through LDS 64 at a time (one coalesced read of the chunk; lane r then
+//     forms row r's residual and barrier weights, which reach the other lanes through LDS);
+//   * the system is factorised in LDS (Jacobi-scaled right-looking Cholesky, pivots floored
+//     at 1e-13; lane i owns row i) and solved by column sweeps.
+// Padded coordinates (d <= j < DP) carry x_j = 0, a unit diagonal and no barrier term, so
+// their steps are 0.  This is a compute kernel: ≈50–100 Newton passes over each prefix's
+// rows (from L2), bound by the VALU.
+#include "ocx_internal.h"
+#include "ocx_sim_kernels.h"
+
+namespace {
+
+constexpr int kMaxIter = 300;
+constexpr double kMu0 = 1.0;
+constexpr double kMuEnd = 1e-10;
+constexpr double kKappa = 10.0;
+constexpr double kTolCenter = 1.0;
+constexpr double kTolFinal = 1e-6;
+constexpr int kFinalSteps = 6;
+constexpr double kPivotFloor = 1e-13;
+constexpr double kBreakdown = 1e8;
+constexpr int RC = 64;  // rows per staged chunk
+
+__device__ __forceinline__ double wsum(double v) { return ocx_seq_sum<64>(v); }
+
+// element (i, j) of sequence b's rows: row-major z [B][T][d] or the tiled layout
+struct WideSrc {
+    const double* z;
+    const double* y;
+    int64_t T, G;
+    int d, P, C, S, tiled;
+    __device__ __forceinline__ double zat(int64_t b, int64_t i, int j) const {
+        if (!tiled) return z[(b * T + i) * d + j];
+        const int64_t g = b / S;
+        const int s = (int)(b - g * S);
+        const int jl = j / C, jj = j - jl * C;
+        return z[((int64_t)(jj >> 1) * G + g) * T * 128 + i * 128 + 2 * (s * P + jl) + (jj & 1)];
+    }
+    __device__ __forceinline__ double yat(int64_t b, int64_t i) const {
+        if (!tiled) return y[b * T + i];
+        const int64_t g = b / S;
+        return y[(g * T + i) * S + (b - g * S)];
+    }
+};
+
+template <int DP, int NORM>
+__global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
+    WideSrc rs, int64_t B, int64_t NP, double* __restrict__ actions, double* __restrict__ obj_out,
+    double* __restrict__ gap_out, double* __restrict__ step_loss, int32_t* __restrict__ info_out) {
+    constexpr int BS = DP / 8;       // block edge per lane
+    constexpr int LD = DP + 1;       // LDS row stride (odd: conflict-free columns and rows)
+    extern __shared__ double lds[];
+    double* M = lds;                 // [RC][LD] row chunk, then [DP][LD] the system
+    double* xs = M + RC * LD;        // x (then the direction vector of a rank-1 term)
+    double* gw = xs + 64;            // row weights r/s
+    double* hw = gw + 64;            // row weights μ/(s·rt)
+    double* vv = hw + 64;            // rank-1 / diagonal terms of the ball barrier
+    double* sc = vv + 64;            // Jacobi scales
+
+    const int lane = threadIdx.x & 63;
+    const int64_t p = blockIdx.x;
+    if (p >= B * NP) return;
+    const int d = rs.d;
+    const int64_t T = rs.T;
+    const int64_t b = p % B;
+    const int64_t n = T - p / B;  // longest problems first
+    const int64_t slot = NP == 1 ? 0 : n;
+    const bool cj = lane < d;     // this lane's coordinate is real
+    const int bj = lane >> 3, bk = lane & 7;
+
+    double x = 0.0, u = (NORM == 1 && cj) ? 0.5 / d : 0.0;
+    double mu = kMu0;
+    int it = 0, kend = 0;
+    bool conv = n == 0, broke = false;
+
+    // Stage rows [c0, c0 + rows) into M (zero-padded to DP columns) and y into yv (lane r).
+    auto stage = [&](int64_t c0, int rows, double& yv) {
+        const int tot = rows * d;
+        for (int f = lane; f < tot; f += 64) {
+            const int r = f / d, j = f - r * d;
+            M[r * LD + j] = rs.zat(b, c0 + r, j);
+        }
+        if (DP > d)
+            for (int f = lane; f < rows * (DP - d); f += 64) {
+                const int r = f / (DP - d), j = d + (f - r * (DP - d));
+                M[r * LD + j] = 0.0;
+            }
+        yv = lane < rows ? rs.yat(b, c0 + lane) : 0.0;
+    };
+    // row r's residual z_r·x − y_r (lane r), in _dot's order from −y
+    auto residual = [&](int r, double yv) {
+        double rr = -yv;
+        for (int j = 0; j < d; ++j) rr = __builtin_fma(M[r * LD + j], xs[j], rr);
+        return rr;
+    };
+
+    while (!conv && it < kMaxIter) {
+        ++it;
+        xs[lane] = x;
+        double Gj = 0.0;
+        double H[BS][BS];
+#pragma unroll
+        for (int i = 0; i < BS; ++i)
+#pragma unroll
+            for (int k = 0; k < BS; ++k) H[i][k] = 0.0;
+        for (int64_t c0 = 0; c0 < n; c0 += RC) {
+            const int rows = (int)(n - c0 < RC ? n - c0 : RC);
+            double yv;
+            stage(c0, rows, yv);
+            double g1 = 0.0, h1 = 0.0;
+            if (lane < rows) {
+                const double r = residual(lane, yv);
+                const double rt = sqrt(__builtin_fma(mu, mu, r * r));
+                const double s = mu + rt;
+                const double inv = 1.0 / (s * rt);
+                g1 = r * rt * inv;  // r / s
+                h1 = mu * inv;      // μ / (s·rt)
+            }
+            gw[lane] = g1;
+            hw[lane] = h1;
+            for (int r = 0; r < rows; ++r) {
+                Gj = __builtin_fma(gw[r], M[r * LD + (lane < DP ? lane : 0)], Gj);
+                double a1[BS], a2[BS];
+#pragma unroll
+                for (int i = 0; i < BS; ++i) {
+                    a1[i] = hw[r] * M[r * LD + bj * BS + i];
+                    a2[i] = M[r * LD + bk * BS + i];
+                }
+#pragma unroll
+                for (int i = 0; i < BS; ++i)
+#pragma unroll
+                    for (int k = 0; k < BS; ++k) H[i][k] = __builtin_fma(a1[i], a2[k], H[i][k]);
+            }
+        }
+        const double im = 1.0 / mu;
+        Gj = cj ? Gj * im : 0.0;
+#pragma unroll
+        for (int i = 0; i < BS; ++i)
+#pragma unroll
+            for (int k = 0; k < BS; ++k) H[i][k] *= im;
+
+        // ---- the ball's barrier: gradient (lane j), diagonal (vv) and a rank-1 term
+        // (xs = its vector, c1 its weight), then the system into M
+        double c1 = 0.0, gu = 0.0, ia = 0.0, be = 0.0, gam = 0.0;
+        double rhs_g;  // right-hand side of the x system
+        if constexpr (NORM == 0) {
+            const double q = 1.0 - wsum(cj ? x * x : 0.0);
+            const double iq = 1.0 / q;
+            Gj = cj ? __builtin_fma(2.0 * iq, x, Gj) : 0.0;
+            vv[lane] = cj ? 2.0 * iq : 1.0;  // padded coordinates: unit diagonal
+            c1 = 4.0 * iq * iq;
+            xs[lane] = cj ? x : 0.0;
+            rhs_g = Gj;
+        } else if constexpr (NORM == 2) {
+            const double iq = cj ? 1.0 / __builtin_fma(-x, x, 1.0) : 0.0;
+            Gj = cj ? __builtin_fma(2.0 * x, iq, Gj) : 0.0;
+            vv[lane] = cj ? 2.0 * __builtin_fma(x, x, 1.0) * iq * iq : 1.0;
+            xs[lane] = 0.0;
+            rhs_g = Gj;
+        } else {
+            const double su = wsum(cj ? u : 0.0);
+            const double iw = 1.0 / (1.0 - su), c = iw * iw;
+            double al = 1.0;
+            if (cj) {
+                const double ip = 1.0 / (u - x), ipp = 1.0 / (u + x);
+                Gj += ip - ipp;
+                gu = iw - ip - ipp;
+                al = __builtin_fma(ip, ip, ipp * ipp);
+                be = (ipp - ip) * (ipp + ip);
+                ia = 1.0 / al;
+            }
+            gam = c / __builtin_fma(c, wsum(ia), 1.0);
+            const double t = wsum(gu * ia);
+            const double hg = (gu - gam * t) * ia;
+            rhs_g = cj ? __builtin_fma(-be, hg, Gj) : 0.0;
+            const double v = be * ia;
+            vv[lane] = cj ? __builtin_fma(-be, v, al) : 1.0;
+            xs[lane] = v;
+            c1 = gam;
+        }
+        // H + diag(vv) + c1·xs xsᵀ into M (full matrix)
+#pragma unroll
+        for (int i = 0; i < BS; ++i) {
+            const int gi = bj * BS + i;
+#pragma unroll
+            for (int k = 0; k < BS; ++k) {
+                const int gk = bk * BS + k;
+                double h = gi < d && gk < d ? H[i][k] : 0.0;
+                h = __builtin_fma(c1 * xs[gi], xs[gk], h);
+                if (gi == gk) h += vv[gi];
+                M[gi * LD + gk] = h;
+            }
+        }
+        // Jacobi scaling, then Cholesky (lane i owns row i)
+        const int ri = lane < DP ? lane : DP - 1;
+        const double dg = M[ri * LD + ri];
+        const double sci = 1.0 / sqrt(dg > 0.0 ? dg : kPivotFloor);
+        sc[lane] = sci;
+        if (lane < DP)
+            for (int j = 0; j <= lane; ++j) M[lane * LD + j] *= sci * sc[j];
+        for (int k = 0; k < DP; ++k) {
+            double s = M[k * LD + k];
+            s = s > kPivotFloor ? s : kPivotFloor;
+            const double l = sqrt(s), rd = 1.0 / l;
+            double lik = 0.0;
+            if (lane == k) M[k * LD + k] = l;
+            if (lane > k && lane < DP) {
+                lik = M[lane * LD + k] * rd;
+                M[lane * LD + k] = lik;
+            }
+            if (lane > k && lane < DP)
+                for (int j = k + 1; j <= lane; ++j)
+                    M[lane * LD + j] = __builtin_fma(-lik, M[j * LD + k], M[lane * LD + j]);
+        }
+        // L w = rhs·sc ; Lᵀ v = −w ; dx = v·sc
+        double vcur = lane < DP ? rhs_g * sci : 0.0, w = 0.0;
+        for (int k = 0; k < DP; ++k) {
+            const double wk = ocx_readlane(vcur, k) / M[k * LD + k];
+            if (lane == k) w = wk;
+            if (lane > k && lane < DP) vcur = __builtin_fma(-M[lane * LD + k], wk, vcur);
+        }
+        double vb = -w, dx = 0.0;
+        for (int k = DP - 1; k >= 0; --k) {
+            const double dk = ocx_readlane(vb, k) / M[k * LD + k];
+            if (lane == k) dx = dk;
+            if (lane < k) vb = __builtin_fma(-M[k * LD + lane], dk, vb);
+        }
+        dx = cj ? dx * sci : 0.0;
+        double du = 0.0, lam2;
+        if constexpr (NORM == 1) {
+            const double rhs = cj ? __builtin_fma(-be, dx, -gu) : 0.0;
+            const double tr = wsum(rhs * ia);
+            du = cj ? (rhs - gam * tr) * ia : 0.0;
+            lam2 = wsum(__builtin_fma(-Gj, dx, -gu * du));
+        } else {
+            lam2 = wsum(-Gj * dx);
+        }
+        const double lam = sqrt(lam2 > 0.0 ? lam2 : 0.0);
+        if (lam > kBreakdown) {  // μ has outrun fp64 (see ocx_exact_ball.hip)
+            broke = true;
+            break;
+        }
+        double step = lam > 0.25 ? 1.0 / (1.0 + lam) : 1.0;
+        for (int h = 0; h < 60; ++h) {
+            const double xn = __builtin_fma(step, dx, x);
+            const double un = NORM == 1 ? __builtin_fma(step, du, u) : 0.0;
+            bool ok;
+            if constexpr (NORM == 0) {
+                ok = wsum(cj ? xn * xn : 0.0) < 1.0;
+            } else if constexpr (NORM == 2) {
+                ok = __ballot(cj && !(fabs(xn) < 1.0)) == 0;
+            } else {
+                ok = __ballot(cj && !(fabs(xn) < un)) == 0 && wsum(cj ? un : 0.0) < 1.0;
+            }
+            if (ok) {
+                x = xn;
+                u = un;
+                break;
+            }
+            step *= 0.5;
+        }
+        if (mu > kMuEnd) {
+            if (lam < kTolCenter) mu = fmax(mu / kKappa, kMuEnd);
+        } else if (lam < kTolFinal || ++kend >= kFinalSteps) {
+            conv = true;
+            break;
+        }
+    }
+
+    // ---- certificate (as ocx_exact_ball.hip): obj, dual bounds of λ_a = r/(2s) and λ_b
+    xs[lane] = x;
+    double P = 0.0, Ya = 0.0, Yb = 0.0, Wa = 0.0, Wb = 0.0;
+    for (int64_t c0 = 0; c0 < n; c0 += RC) {
+        const int rows = (int)(n - c0 < RC ? n - c0 : RC);
+        double yv;
+        stage(c0, rows, yv);
+        double la = 0.0, lb = 0.0;
+        if (lane < rows) {
+            const double r = residual(lane, yv);
+            P += 0.5 * fabs(r);
+            const double s = mu + sqrt(__builtin_fma(mu, mu, r * r));
+            la = 0.5 * r / s;
+            lb = fabs(r) > 1e3 * mu ? (r > 0.0 ? 0.5 : -0.5) : la;
+            Ya = __builtin_fma(la, yv, Ya);
+            Yb = __builtin_fma(lb, yv, Yb);
+        }
+        gw[lane] = la;
+        hw[lane] = lb;
+        for (int r = 0; r < rows; ++r) {
+            const double a = M[r * LD + (lane < DP ? lane : 0)];
+            Wa = __builtin_fma(gw[r], a, Wa);
+            Wb = __builtin_fma(hw[r], a, Wb);
+        }
+    }
+    P = wsum(P);
+    Ya = wsum(Ya);
+    Yb = wsum(Yb);
+    if (!cj) Wa = Wb = 0.0;
+    double na, nb;
+    if constexpr (NORM == 0) {
+        na = sqrt(wsum(Wa * Wa));
+        nb = sqrt(wsum(Wb * Wb));
+    } else if constexpr (NORM == 2) {
+        na = wsum(fabs(Wa));
+        nb = wsum(fabs(Wb));
+    } else {
+        double ma = fabs(Wa), mb = fabs(Wb);
+        for (int o = 32; o > 0; o >>= 1) {
+            ma = fmax(ma, __shfl_xor(ma, o, 64));
+            mb = fmax(mb, __shfl_xor(mb, o, 64));
+        }
+        na = ma;
+        nb = mb;
+    }
+    const double bound = fmax(fmax(-Ya - na, -Yb - nb), 0.0);
+    if (cj) actions[(b * NP + slot) * d + lane] = x;
+    if (lane == 0) {
+        if (obj_out) obj_out[b * NP + slot] = P;
+        if (gap_out) gap_out[b * NP + slot] = fmax(P - bound, 0.0);
+        if (info_out)
+            info_out[b * NP + slot] = broke ? (OCX_EXACT_INFO_BREAKDOWN | it) : (conv ? it : -it);
+        if (step_loss) {
+            // FTL's loss at step n (replay_exact_ftl :318-323: _dot's sequential sum)
+            double lo = 0.0;
+            if (n < T) {
+                double q = 0.0;
+                for (int j = 0; j < d; ++j) q = q + rs.zat(b, n, j) * xs[j];
+                lo = 0.5 * fabs(q - rs.yat(b, n));
+            }
+            step_loss[b * NP + slot] = lo;
+        }
+    }
+}
+
+template <int DP, int NORM>
+hipError_t launch_wide_dn(const WideSrc& rs, int64_t B, int64_t NP, double* actions, double* obj,
+                          double* gap, double* step_loss, int32_t* info, hipStream_t st) {
+    const size_t lds = (size_t)(RC * (DP + 1) + 5 * 64) * sizeof(double);
+    hipLaunchKernelGGL((ocx_exact_wide_kernel<DP, NORM>), dim3((unsigned)(B * NP)), dim3(64), lds,
+                       st, rs, B, NP, actions, obj, gap, step_loss, info);
+    return hipGetLastError();
+}
+
+template <int DP>
+hipError_t launch_wide_d(const WideSrc& rs, int64_t B, int64_t NP, int norm, double* actions,
+                         double* obj, double* gap, double* step_loss, int32_t* info,
+                         hipStream_t st) {
+    switch (norm) {
+        case 0: return launch_wide_dn<DP, 0>(rs, B, NP, actions, obj, gap, step_loss, info, st);
+        case 1: return launch_wide_dn<DP, 1>(rs, B, NP, actions, obj, gap, step_loss, info, st);
+        case 2: return launch_wide_dn<DP, 2>(rs, B, NP, actions, obj, gap, step_loss, info, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+// 10 < d <= 64, row-major (tiled = 0) or the tiled layout (P, C, S, G of it)
+hipError_t ocx_launch_exact_wide(const double* z, const double* y, int64_t B, int64_t T,
+                                 int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
+                                 int all_prefixes, double* actions, double* obj, double* gap,
+                                 double* step_loss, int32_t* info, hipStream_t st) {
+    const int64_t NP = all_prefixes ? T + 1 : 1;
+    if (B == 0 || NP == 0) return hipSuccess;
+    if (d < 1 || d > 64 || B * NP > 0x7fffffffLL) return hipErrorInvalidValue;
+    const WideSrc rs{z, y, T, G, (int)d, P, C, S, tiled};
+    if (d <= 16) return launch_wide_d<16>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
+    if (d <= 32) return launch_wide_d<32>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
+    return launch_wide_d<64>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
+}

@@ -39,6 +39,12 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
                                      hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
                                      void* fold_arg, int wps, int64_t sub_seqs, int cand,
                                      hipStream_t st);
+// the general exact comparator for 10 < d <= 64 (ocx_exact_wide.hip): row-major z/y
+// (tiled = 0) or a tiled layout's (P, C, S, G)
+hipError_t ocx_launch_exact_wide(const double* z, const double* y, int64_t B, int64_t T,
+                                 int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
+                                 int all_prefixes, double* actions, double* obj, double* gap,
+                                 double* step_loss, int32_t* info, hipStream_t st);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

@@ -98,16 +98,19 @@ def test_exact_driver_loop_body(ef):
 
 def test_out_of_regime_general(ef):
     """Outside the closed form's regime the drop-in takes the general solver (round 2
-    raised NotImplementedError; tests/test_gpu_exact_general.py checks the answers); only
-    d > 10 there is unsupported."""
+    raised NotImplementedError; tests/test_gpu_exact_general.py checks the answers); d = 11
+    (beyond round 3's limit) now answers too, only d > 64 is unsupported."""
     z, y, _ = O.random_iid_sample(2025, 50, 0)
     a = ef.compute_prefix_actions(ef.ExactFTLNoClip(5, 50), 3.0 * z, y)
     assert a.shape == (51, 5) and np.all(np.linalg.norm(a, axis=1) <= 1.0 + 1e-12)
     x = ef.ExactFTLNoClip(5, 50).solve_prefix_from_full(z, 0.5 * y, 50)
     assert np.linalg.norm(x) <= 1.0 + 1e-12
     zz = 3.0 * np.random.default_rng(0).standard_normal((20, 11))
+    a11 = ef.compute_prefix_actions(ef.ExactFTLNoClip(11, 20), zz, np.ones(20))
+    assert a11.shape == (21, 11) and np.all(np.linalg.norm(a11, axis=1) <= 1.0 + 1e-12)
+    zz = 3.0 * np.random.default_rng(0).standard_normal((20, 65))
     with pytest.raises(NotImplementedError):
-        ef.compute_prefix_actions(ef.ExactFTLNoClip(11, 20), zz, np.ones(20))
+        ef.compute_prefix_actions(ef.ExactFTLNoClip(65, 20), zz, np.ones(20))
 
 
 def test_prefix_actions_batch_lane_splits(ef):

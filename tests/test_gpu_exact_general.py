@@ -213,10 +213,91 @@ def test_exact_driver_linf(eng):
 
 
 def test_general_limits_are_loud(eng):
-    z, y = _data(1, 2, 10, 11, clip=False)
+    z, y = _data(1, 2, 10, 65, clip=False)
     with pytest.raises(NotImplementedError):
         eng.exact_ball_solve(z, y, norm="linf")
     with pytest.raises(NotImplementedError):
         eng.ftl_exact_batch(z, y, norm="linf")
     with pytest.raises(ValueError):
         eng.exact_ball_solve(z[..., :3], y, norm="l3")
+
+
+# ---- 10 < d <= 64: the LDS-resident system (ocx_exact_wide.hip) -------------------------
+@pytest.mark.parametrize("norm", ["linf", "l1"])
+@pytest.mark.parametrize("d,T,clip,labels", [(16, 40, True, "pm1"), (16, 30, False, "real"),
+                                             (64, 80, True, "pm1"), (33, 50, False, "pm1")])
+def test_wide_lp_matches_highs(eng, norm, d, T, clip, labels):
+    """configs[2]'s d = 64 (and 16, 33) outside the closed forms: the linf ball on the
+    reference's clipped rows, unclipped rows, real labels — against HiGHS, with the
+    certificate.  Parity with cvxpy: unpinned."""
+    B = 2
+    z, y = _data(7 * d + (norm == "l1"), B, T, d, clip=clip, labels=labels)
+    res = eng.exact_ball_solve(z, y, norm=norm, all_prefixes=True)
+    assert res["actions"].shape == (B, T + 1, d)
+    for b in range(B):
+        assert np.all(res["actions"][b, 0] == 0.0)
+        for n in (1, 2, d // 2, d, d + 1, T):
+            x_lp, f_lp = lp_solve(z[b, :n], y[b, :n], norm)
+            x = res["actions"][b, n]
+            f = res["obj"][b, n]
+            assert _norm_of(x, norm) <= 1.0 + 1e-12
+            assert abs(objective(z[b, :n], y[b, :n], x) - f) <= 1e-11 * (1.0 + f)
+            assert abs(f - f_lp) <= 1e-7 * (1.0 + f_lp), (b, n, f, f_lp)
+            _check_certificate(res, f_lp, b, n)
+        for n in (0, d, T - 1):
+            q = 0.0
+            for j in range(d):
+                q = q + z[b, n, j] * res["actions"][b, n, j]
+            assert res["step_loss"][b, n] == 0.5 * abs(q - y[b, n])
+
+
+@pytest.mark.parametrize("d", [16, 40])
+def test_wide_l2_vs_slsqp(eng, d):
+    B, T = 2, 30
+    z, y = _data(90 + d, B, T, d, clip=True, labels="real")
+    z *= 2.5                                                      # rows outside the ball
+    res = eng.exact_ball_solve(z, y, norm="l2")
+    for b in range(B):
+        for n in (2, T // 2, T):
+            x_s, f_s = socp_solve(z[b, :n], y[b, :n])
+            f = res["obj"][b, n]
+            assert np.linalg.norm(res["actions"][b, n]) <= 1.0 + 1e-12
+            assert f <= f_s + 1e-9 * (1.0 + f_s), (b, n)          # no worse than SLSQP
+            _check_certificate(res, f_s, b, n)
+
+
+def test_wide_tiled_and_engine_paths(eng):
+    """d = 64: the tiled entry point equals the row-major one bit for bit, and the batched
+    FTRL-vs-exact paths (host arrays and DeviceBatch.ftrl_vs_exact_general, which now solves
+    only the sequences outside the regime) agree, with every solve certified."""
+    import torch
+    B, T, d = 10, 40, 64
+    z, y = _data(21, B, T, d, clip=True)
+    ref = eng.exact_ball_solve(z, y, norm="linf")
+    db = eng.DeviceBatch(B, T, d).pack(z, y)
+    g = db.exact_general("linf")
+    torch.cuda.synchronize()
+    for k in ("actions", "obj", "gap", "step_loss", "info"):
+        assert np.array_equal(g[k][:B].cpu().numpy(), ref[k]), k
+    host = eng.ftrl_vs_exact_batch(z, y, SQ2, norm="linf")
+    assert not host["in_regime"].any() and host["exact_gap_max"] < 1e-5
+    want_cum = np.cumsum(ref["step_loss"][:, :T], axis=1)[:, -1]
+    assert np.array_equal(host["cum_exact"], want_cum)
+    assert np.array_equal(host["comp"], ref["obj"][:, T])
+    db2 = eng.DeviceBatch(B, T, d).pack(z, y)
+    rg = db2.ftrl_vs_exact_general(SQ2, norm="linf")
+    torch.cuda.synchronize()
+    assert not rg[:B].cpu().numpy().any()
+    assert np.array_equal(db2.cum_exact[:B].cpu().numpy(), want_cum)
+    assert np.array_equal(db2.comp[:B].cpu().numpy(), ref["obj"][:, T])
+    assert db2.exact_gap_max < 1e-5
+
+
+def test_uncertified_solve_raises(eng, monkeypatch):
+    """A solve whose certificate is not within the tolerance makes every engine path raise
+    RuntimeError (exact_ftl.py:125-126 raises on a solver failure) instead of returning it."""
+    from online_convex_optimization_amd import engine as E
+    z, y = _data(4, 2, 20, 5, clip=False)
+    monkeypatch.setattr(E, "EXACT_GAP_RTOL", -1.0)  # no gap passes
+    with pytest.raises(RuntimeError, match="did not certify"):
+        E.ftl_exact_batch(z, y, norm="linf")
