@@ -361,6 +361,45 @@ __device__ __forceinline__ void ocx_action_exact_poly(const double (&th)[C], dou
         x[j] = (best > 0.0 && c * C + j == bj) ? (th[j] > 0.0 ? -1.0 : 1.0) : 0.0;
 }
 
+// Prefixes where the closed form's maximiser of x·S_t is not unique AND the general solver's
+// answer — the central path's limit, the analytic centre of the optimal face
+// (ocx_exact_ball.hip), what interior-point cvxpy backends approach — is not the closed
+// form's point:
+//   l1    two or more coordinates attain max_j |S_j| > 0 (the face is their simplex; the
+//         rows' slack terms place its centre);
+//   linf  S_j = 0 in a coordinate some row of the prefix has touched (`touch`, bit j: the
+//         face is free there, and the rows pull its centre off 0).
+// S_t = 0 is not such a case: the centre is then x = 0 (the rows' barrier has gradient −S_t
+// = 0 there), which is the closed forms' answer.  Callers leave the regime on a tie, so the
+// general solver answers those sequences.  Whole wave active (lane exchanges).
+template <int C, int P>
+__device__ __forceinline__ bool ocx_exact_poly_tie(const double (&th)[C], uint64_t touch, int norm) {
+    if (norm == 1) {
+        double best = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) best = fmax(best, fabs(th[j]));
+#pragma unroll
+        for (int m = 1; m < P; m <<= 1) best = fmax(best, __shfl_xor(best, m, 64));
+        double cnt = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) cnt += (best > 0.0 && fabs(th[j]) == best) ? 1.0 : 0.0;
+        return ocx_seq_sum<P>(cnt) >= 2.0;
+    }
+    if (norm == 2) {
+        double f = 0.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) f += (th[j] == 0.0 && ((touch >> j) & 1ull)) ? 1.0 : 0.0;
+        return ocx_seq_sum<P>(f) > 0.0;
+    }
+    return false;
+}
+template <int C>
+__device__ __forceinline__ uint64_t ocx_touch(uint64_t touch, const ocx_d2* z) {
+#pragma unroll
+    for (int j = 0; j < C; ++j) touch |= (ocx_zj(z, j) != 0.0 ? 1ull : 0ull) << j;
+    return touch;
+}
+
 // Is row z inside the regime of the `norm` ball's closed form: its dual norm <= 1
 // (l2: ||z||_2^2 <= 1 + 1e-6, the bar of round 1; l1 ball: max_j |z_j| <= 1 + 1e-12;
 // linf ball: sum_j |z_j| <= 1 + 1e-12)?  Every lane of the sequence gets the answer.

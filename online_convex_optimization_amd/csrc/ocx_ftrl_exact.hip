@@ -92,6 +92,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
 #pragma unroll
     for (int j = 0; j < C; ++j) tr[j] = te[j] = 0.0;
     bool linear = true;
+    uint64_t touch = 0;  // linf: coordinates some row has touched (ocx_exact_poly_tie)
     bool clipped = true;  // every ‖z_t‖² <= 1 + 1e-12 (closed-form comparators)
 
     ocx_d2 zb[NB][K];
@@ -145,6 +146,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
                     for (int j = 0; j < C; ++j) xe[j] = (tot[2] == 0.0) ? 0.0 : sce * te[j];
                 } else {
                     ocx_action_exact_poly<C, P>(te, xe, norm, lane);
+                    linear = linear && !ocx_exact_poly_tie<C, P>(te, touch, norm);
                 }
                 const double qe = ocx_zdot<C, P, CHAIN>(z, xe, lane);
                 const double dr = qr - yv;
@@ -154,6 +156,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
                     linear = linear && tot[3] <= 1.0 + 1e-6 && fabs(yv) == 1.0;
                 } else {
                     linear = linear && ocx_dual_ok<C, P, CHAIN>(z, norm, lane) && fabs(yv) == 1.0;
+                    if (norm == 2) touch = ocx_touch<C>(touch, z);
                 }
                 clipped = clipped && tot[3] <= 1.0 + 1e-12;
                 const double gr = ocx_grad(dr);
@@ -173,6 +176,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_ftrl_exact_kernel(
         ocx_action_ftl<C, P, CHAIN>(te, xs, lane);
     } else {
         ocx_action_exact_poly<C, P>(te, xs, norm, lane);
+        linear = linear && !ocx_exact_poly_tie<C, P>(te, touch, norm);
     }
     if (comp_f != nullptr) {
         ocx_action_ftl<C, P, CHAIN>(tr, xf, lane);

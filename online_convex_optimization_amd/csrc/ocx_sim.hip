@@ -65,6 +65,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
     const bool ftl = (algo != 0);
     const bool exact = (algo == 2);
     bool linear = true;  // algo 2: data inside the closed form's regime so far
+    uint64_t touch = 0;  // algo 2, linf: coordinates some row has touched (ocx_exact_poly_tie)
     bool clean = true;   // onepass: every sub-gradient so far was −y_t/2 (see below)
 
     double th[C];
@@ -101,6 +102,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 } else {
                     if (exact && norm != 0) {
                         ocx_action_exact_poly<C, P>(th, x, norm, lane);
+                        linear = linear && !ocx_exact_poly_tie<C, P>(th, touch, norm);
                     } else {
                         ocx_action_ftl<C, P, CHAIN>(th, x, lane);
                     }
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
                 if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
                     linear = linear && ocx_dual_ok<C, P, CHAIN>(zb[u], norm, lane) &&
                              fabs(yb[u]) == 1.0;
+                    if (norm == 2) touch = ocx_touch<C>(touch, zb[u]);
                     gq = -yb[u];
                 }
 #pragma unroll
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         }
     } else if (exact && norm != 0) {
         ocx_action_exact_poly<C, P>(th, xs, norm, lane);
+        linear = linear && !ocx_exact_poly_tie<C, P>(th, touch, norm);
     } else {
         ocx_action_ftl<C, P, CHAIN>(th, xs, lane);
     }
@@ -369,10 +373,12 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
 #pragma unroll
     for (int j = 0; j < C; ++j) th[j] = 0.0;
     bool linear = true;
+    uint64_t touch = 0;
     for (int64_t t = 0; t <= T; ++t) {
         double x[C];
         if (norm != 0) {
             ocx_action_exact_poly<C, P>(th, x, norm, lane);
+            linear = linear && !ocx_exact_poly_tie<C, P>(th, touch, norm);
         } else {
             ocx_action_ftl<C, P, CHAIN>(th, x, lane);
         }
@@ -386,6 +392,7 @@ __global__ __launch_bounds__(OCX_BLOCK) void ocx_prefix_actions_kernel(
         ocx_load_tile<C>(z, zp + t * tstride, kst);
         const double yv = yp[t * S];
         linear = linear && ocx_dual_ok<C, P, CHAIN>(z, norm, lane) && fabs(yv) == 1.0;
+        if (norm == 2) touch = ocx_touch<C>(touch, z);
         const double gq = -yv;
 #pragma unroll
         for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(z, j);

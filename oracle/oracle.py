@@ -155,6 +155,20 @@ def _poly_action(theta: np.ndarray, norm: str) -> np.ndarray:
     return x
 
 
+def _poly_tie(theta: np.ndarray, touched: np.ndarray, norm: str) -> bool:
+    """Prefixes whose LP optimum is a face the closed form does not centre (kernels:
+    ocx_exact_poly_tie): l1 with two or more coordinates at max |S_j| > 0; linf with S_j = 0
+    in a coordinate some row of the prefix touched.  The engine answers those sequences with
+    the general solver (the analytic centre of the face, as interior-point cvxpy backends)."""
+    if norm == "l1":
+        a = np.abs(theta)
+        m = float(a.max(initial=0.0))
+        return m > 0.0 and int((a == m).sum()) >= 2
+    if norm == "linf":
+        return bool(np.any((theta == 0.0) & touched))
+    return False
+
+
 def _dual_ok(zt: np.ndarray, norm: str) -> bool:
     if norm == "l1":
         return float(np.max(np.abs(zt), initial=0.0)) <= 1.0 + 1e-12
@@ -183,13 +197,17 @@ def ftl_exact_poly(z, y, norm: str):
     acts = np.zeros((T + 1, d))
     cum = 0.0
     ok = True
+    touched = np.zeros(d, dtype=bool)
     for t in range(T):
         x = _poly_action(th, norm)
         acts[t] = x
+        ok = ok and not _poly_tie(th, touched, norm)
         cum += 0.5 * abs(_seqdot(z[t], x) - y[t])
         ok = ok and _dual_ok(z[t], norm) and abs(y[t]) == 1.0
+        touched |= z[t] != 0.0
         th = th + (-y[t]) * z[t]
     xs = _poly_action(th, norm)
+    ok = ok and not _poly_tie(th, touched, norm)
     acts[T] = xs
     comp = 0.0
     for t in range(T):

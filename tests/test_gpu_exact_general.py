@@ -301,3 +301,37 @@ def test_uncertified_solve_raises(eng, monkeypatch):
     monkeypatch.setattr(E, "EXACT_GAP_RTOL", -1.0)  # no gap passes
     with pytest.raises(RuntimeError, match="did not certify"):
         E.ftl_exact_batch(z, y, norm="linf")
+
+
+@pytest.mark.parametrize("norm", ["l1", "linf"])
+def test_tied_prefixes_take_the_general_solvers_centre(eng, norm):
+    """Constructed ties (exact_ftl.py:119-128 leaves the choice to cvxpy): rows alternating
+    e_1, e_2 with +1 labels make |S_1| = |S_2| at every even prefix (l1), and a coordinate
+    touched by rows of both signs returns to S_j = 0 (linf).  The closed form would play the
+    first coordinate / 0 there; such sequences now leave the closed form's regime and the
+    engine answers with the general solver — the analytic centre of the optimal face, the
+    interior-point limit — so the batched closed-form path and the general solver give the
+    same actions, at the LP optimum."""
+    T, d = 24, 5
+    z = np.zeros((2, T, d))
+    y = np.ones((2, T))
+    z[0, 0::2, 0] = 1.0
+    z[0, 1::2, 1] = 1.0
+    z[1, :, 2] = 0.5                       # a sequence without ties: stays closed form
+    z[1, :, 3] = 0.25
+    if norm == "linf":
+        z[0, 1::2, 1] = 0.0
+        z[0, :, 0] = 0.5
+        y[0, 1::2] = -1.0                  # S_1 returns to 0 every second step
+    raw, ok_raw = eng.ftl_prefix_actions_batch(z, y, norm=norm, check_regime=False)
+    assert list(ok_raw) == [False, True]
+    acts, ok = eng.ftl_prefix_actions_batch(z, y, norm=norm)
+    gen = eng.exact_ball_solve(z[:1], y[:1], norm=norm)
+    assert np.array_equal(acts[0], gen["actions"][0])        # the general solver's answer
+    assert np.array_equal(acts[1], raw[1])                   # untied: the closed form
+    for n in range(1, T + 1):
+        _, f_lp = lp_solve(z[0, :n], y[0, :n], norm)
+        assert abs(objective(z[0, :n], y[0, :n], acts[0, n]) - f_lp) <= 1e-8 * (1.0 + f_lp)
+    cum, comp, act, in_regime = eng.ftl_exact_batch(z, y, norm=norm)
+    assert list(in_regime) == [False, True]
+    assert np.array_equal(act[0], gen["actions"][0, T])
