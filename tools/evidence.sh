@@ -1,0 +1,70 @@
+#!/bin/bash
+# The one recipe behind the numbers in DESIGN.md §5 and profiles/ (run on the GPU box through
+# gpurun, from the repository root).  Usage:
+#
+#   tools/evidence.sh TAG STEP [STEP ...]
+#
+# Every step writes gpurun_out/TAG_<step>.* and ends the script at the first failure other
+# than failing tests (pytest exit 1), so a crash, abort or time limit is never followed by
+# more GPU work.  Steps:
+#   suite        pytest -m gpu (one process) and smoke()
+#   bench        the default bench line (python bench.py)
+#   stats        rocprofv3 --kernel-trace --stats of a 20-step bench run (kernel averages)
+#   traffic      two PMC passes (FETCH_SIZE, WRITE_SIZE) over a 2-step bench run, reduced by
+#                tools/pmc_traffic.py (gfx950 x2 read correction) into TAG_traffic.json
+#   gensq        SQ counters of the generator (one 32 768 x 1e4 x 64 launch after a warm-up)
+#   genlds       LDS counters of the generator (instructions, bank conflicts, active cycles)
+#   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
+#   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
+#   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
+#   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
+set -u
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"
+mkdir -p gpurun_out
+TAG="$1"
+shift
+O="$R/gpurun_out/$TAG"
+fail() { echo "$1 failed (rc $2)"; exit "$2"; }
+for step in "$@"; do
+  case "$step" in
+  suite)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "${O}_suite.log" 2>&1
+    rc=$?; tail -1 "${O}_suite.log"
+    [ $rc -eq 0 ] || [ $rc -eq 1 ] || fail suite $rc
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "${O}_smoke.log" 2>&1 || fail smoke $?
+    tail -1 "${O}_smoke.log" ;;
+  bench)
+    timeout -k 10 600 python bench.py > "${O}_bench.log" 2>&1 || fail bench $?
+    grep '^{' "${O}_bench.log" > "${O}_bench.json"; cut -c1-300 "${O}_bench.json" ;;
+  stats)
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "${O}_stats" -o s --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --cpu-seconds 0 --two-pass-steps 0 > "${O}_stats.log" 2>&1) || fail stats $?
+    head -6 "${O}_stats/s_kernel_stats.csv" | cut -c1-160 ;;
+  traffic)
+    for C in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "${O}_pmc_$C" -o pmc -- python3 "$R/bench.py" --steps 2 --warmup 0 --cpu-seconds 0 --two-pass-steps 0 --e2e-steps 1 > "${O}_pmc_$C.log" 2>&1) || fail "pmc $C" $?
+    done
+    python tools/pmc_traffic.py --fetch "${O}_pmc_FETCH_SIZE" --write "${O}_pmc_WRITE_SIZE" --kernel ocx_alg_pipe_kernel --B 32768 --T 10000 --d 64 --P 8 --passes 1 --out "${O}_traffic.json" > /dev/null || fail traffic $?
+    head -c 600 "${O}_traffic.json"; echo ;;
+  gensq)
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d "${O}_gensq" -o sq -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_gensq.log" 2>&1) || fail gensq $?
+    python tools/pmc_summary.py --kernel gen_wave "${O}_gensq" ;;
+  genlds)
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES --output-format csv -d "${O}_genlds" -o lds -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_genlds.log" 2>&1) || fail genlds $?
+    python tools/pmc_summary.py --kernel gen_wave "${O}_genlds" ;;
+  overlap)
+    timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?
+    cut -c1-260 "${O}_overlap.jsonl" ;;
+  pipe)
+    timeout -k 10 400 python -u tools/r04_pipe_probe.py > "${O}_pipe.jsonl" 2> "${O}_pipe.err" || fail pipe $?
+    cut -c1-200 "${O}_pipe.jsonl" ;;
+  overlaptrace)
+    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=3:1:0 timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
+    python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
+    cut -c1-400 "${O}_otrace.json" ;;
+  sweep)
+    timeout -k 10 900 python tools/perf_extra.py sweep config4 > "${O}_sweep.log" 2>&1 || fail sweep $?
+    grep '^{' "${O}_sweep.log" | cut -c1-220 ;;
+  *) echo "unknown step $step"; exit 64 ;;
+  esac
+done

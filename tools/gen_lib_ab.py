@@ -1,7 +1,7 @@
 """Generator A/B (round 3) between tune_r03 libraries named on the command line, the first
 the reference: checks their outputs agree (wrapping int64 sums of z and y, full and strided)
 on three shapes, then times ocx_dev_gen_gT for each (min over rounds, HIP events).
-    python tools/r03_gen_lib_ab.py rej0,rej1"""
+    python tools/gen_lib_ab.py rej0,rej1"""
 import ctypes
 import json
 import os
