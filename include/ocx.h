@@ -419,8 +419,8 @@ int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* str
  * max(0, max over every batch's regrets), bit-identical to the host loop.  Queued on
  * `stream`; complete when the stream reaches this point.
  *   Pipelined (the default where supported: d = 64 with the 8 x 8 or 16 x 4 butterfly
- * layout): the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator
- * round) and sub-batch i+1 is generated while the FTRL kernel reads sub-batch i on a second
+ * layout, and a batch of at least four generator rounds unless sub_seqs > 0 asks for it):
+ * the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator round) and sub-batch i+1 is generated while the FTRL kernel reads sub-batch i on a second
  * stream of the library's, the generator capped at three waves per SIMD and the FTRL kernel
  * in a 128-VGPR form so both stay resident (csrc/ocx_pipeline.hip); consecutive batches
  * overlap the same way.  Same kernels and arithmetic as the sequential path: the regrets are

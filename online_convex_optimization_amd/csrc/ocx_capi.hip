@@ -487,7 +487,8 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
     // the reference's streamed pass (the bit-exact modes)
     const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
-    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L)) {
+    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) &&
+        (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
                                           regret, onepass, acc ? fold_max : nullptr, acc,
                                           pipe_wps(), sub_seqs, pipe_cand_default(), st));
@@ -945,18 +946,44 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             }
         }
         OCX_HIP(cx->out.ensure((size_t)chunk * 8));
-        for (int64_t r0 = 0; r0 < R; r0 += chunk) {
+        // Generation overlapped with FTRL (ocx_pipeline.hip) where the layout allows it
+        // (OCX_PIPELINE=0: the sequential loop below).  For g(T) alone the equal batches go
+        // through one call, so batch k+1's generation overlaps batch k's last FTRL pass too.
+        ocx_layout Lp;
+        if (int rc = ocx_layout_init(chunk, T, d, lanes_per_seq, &Lp)) return rc;
+        const char* pe = std::getenv("OCX_PIPELINE");
+        const bool pipe = (!pe || std::atoi(pe) != 0) && ocx_pipeline_supported(&Lp) &&
+                          ocx_pipeline_worth(&Lp, pipe_wps());
+        int64_t done = 0;
+        if (pipe && dmax) {
+            const int64_t nfull = R / chunk;
+            OCX_HIP(cx->zt.ensure((size_t)Lp.z_elems * 8));
+            OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
+            OCX_HIP(ocx_run_gen_sim_pipelined(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
+                                              cx->yt.as<double>(), eta0, cx->out.as<double>(),
+                                              onepass, fold_max, dmax, pipe_wps(), 0,
+                                              pipe_cand_default(), st));
+            done = nfull * chunk;
+        }
+        for (int64_t r0 = done; r0 < R; r0 += chunk) {
             const int64_t nb = std::min(chunk, R - r0);
             ocx_layout L;
             if (int rc = ocx_layout_init(nb, T, d, lanes_per_seq, &L)) return rc;
             OCX_HIP(cx->zt.ensure((size_t)L.z_elems * 8));
             OCX_HIP(cx->yt.ensure((size_t)L.y_elems * 8));
-            OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
-                                      cx->yt.as<double>(), st));
             double* rdst = regrets_on_device ? regrets + r0 : cx->out.as<double>();
-            OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0, nullptr,
-                                   rdst, nullptr, nullptr, nullptr, st, nullptr, nullptr,
-                                   onepass));
+            if (pipe && ocx_pipeline_supported(&L) && ocx_pipeline_worth(&L, pipe_wps())) {
+                OCX_HIP(ocx_run_gen_sim_pipelined(&L, base_seed, run0 + r0, 1, cx->zt.as<double>(),
+                                                  cx->yt.as<double>(), eta0, rdst, onepass,
+                                                  nullptr, nullptr, pipe_wps(), 0,
+                                                  pipe_cand_default(), st));
+            } else {
+                OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
+                                          cx->yt.as<double>(), st));
+                OCX_HIP(ocx_launch_alg(&L, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0,
+                                       nullptr, rdst, nullptr, nullptr, nullptr, st, nullptr,
+                                       nullptr, onepass));
+            }
             if (dmax) {
                 OCX_HIP(launch_max_fold(cx->out.as<double>(), nb, dmax, st));
             } else if (!regrets_on_device) {

@@ -74,6 +74,18 @@ bool ocx_pipeline_supported(const ocx_layout* L) {
            L->T * L->d < ((int64_t)1 << 32);
 }
 
+// Whether cutting L's batch into generator rounds of `wps` waves per SIMD pays: at least four
+// sub-batches (one round each).  A batch of a round or two (the capacity-limited T = 1e5
+// batches of ~4 900 streams) would leave the generator's last round nearly empty, and one
+// round at full occupancy (ocx_launch_gen_gT) beats two at three waves per SIMD.
+bool ocx_pipeline_worth(const ocx_layout* L, int wps) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return L->G * L->S >= 4 * (int64_t)cus * 4 * std::max(1, wps);
+}
+
 // nbatch batches of L->B runs each (runs run0 + k·B, k < nbatch) through one z/y buffer of
 // layout L; regret[] holds the last batch's regrets, dmax (nullable, device) folds the max
 // over all of them (ocx_max_fold: bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
