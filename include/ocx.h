@@ -195,13 +195,13 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * step_loss [B][NP] (nullable) = ½|z_n·x_n − y_n|, what FTL pays at step n with the prefix-n
  * action (replay_exact_ftl :318-323; 0 for n = T), so Σ_n step_loss is exact FTL's cumulative
  * loss; info [B][NP] (int32, nullable) = the solve's status and Newton steps:
- *   info > 0, bit OCX_EXACT_INFO_BREAKDOWN clear: converged (steps);
+ *   info >= 0, bit OCX_EXACT_INFO_BREAKDOWN clear: converged (steps; 0: the empty prefix);
  *   info < 0: the 300-step cap ended the solve (-steps);
  *   bit OCX_EXACT_INFO_BREAKDOWN set: stopped where μ outran fp64 (a Newton decrement no
  *     centred step produces) at the last centre, after (info & 0xFFFFF) steps — accurate to
  *     that μ only.
  * Only a converged solve is an answer by itself; for the other two the certificate decides
- * (the engine accepts a solve iff info > 0 and gap <= 1e-6·(1 + |obj|), and raises
+ * (the engine accepts a solve iff info >= 0 and gap <= 1e-6·(1 + |obj|), and raises
  * otherwise, as exact_ftl.py:125-126 does on a solver failure).  1 <= d <=
  * OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy: unpinned (validated
  * against scipy's HiGHS LPs and by the certificate). */

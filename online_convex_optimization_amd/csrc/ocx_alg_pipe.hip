@@ -295,16 +295,17 @@ __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
 }
 
 namespace {
-// CAND (candidate actions formed a step early) where one wave's step latency sets the time:
-// launches of at most OCX_PIPE_CAND_MAX_WAVES waves (2 per SIMD by default).  Beyond that
-// the plain pipelined step streams at the HBM ceiling already and the candidates' extra
-// VALU work (two butterflies, a sqrt and a division per step) buys nothing.
-// OCX_PIPE_CAND=0/1 forces either form (tuning, tests; read at every launch).
+// CAND (candidate actions formed a step early): bit-identical, and measured SLOWER on every
+// batch it was meant for (profiles/r04_pipe_probe.jsonl): 4 900 x 1e5 x 64 FTRL 40.4 ->
+// 67.8 ms, FTL 45.8 -> 95.1 ms; 3 328 x 1e5 (16 x 4) FTRL 35.5 -> 56.4 ms; d = 1024 and the
+// bench batch unchanged or 2-3 % slower.  At 0.6 waves per SIMD the step is bound by the
+// wave's instruction issue, not by its dependency chain: the two candidates' butterflies,
+// sqrt and division per step cost more issue slots than the shorter chain saves.  Off by
+// default; OCX_PIPE_CAND=1 selects it (tuning, tests; read at every launch).
 bool pipe_cand(const ocx_layout* L) {
     // read per launch (a getenv per kernel launch is noise), so one process can A/B both
     if (const char* e = std::getenv("OCX_PIPE_CAND")) return std::atoi(e) != 0;
-    const char* m = std::getenv("OCX_PIPE_CAND_MAX_WAVES");
-    return L->G <= (m ? (int64_t)std::atoll(m) : (int64_t)2048);
+    return false;
 }
 
 template <int C, int P, bool FTL, bool CAND>

@@ -465,7 +465,7 @@ int pipe_wps() {
 }
 int pipe_cand_default() {
     const char* e = std::getenv("OCX_PIPE_CAND");
-    return e ? (std::atoi(e) != 0) : 1;
+    return e ? (std::atoi(e) != 0) : 0;
 }
 }  // namespace
 

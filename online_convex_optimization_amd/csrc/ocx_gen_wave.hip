@@ -820,7 +820,7 @@ __device__ __forceinline__ void load_state6(const uint64_t* p, ocx_u128& state, 
 // OV (the overlapped pipeline, ocx_pipeline.hip): four-wave blocks of the default d = 64
 // form, so the launcher can cap the generator at three blocks (waves) per CU (SIMD) through
 // its LDS request and leave each SIMD room for one FTRL wave beside it.
-__host__ __device__ constexpr int gen_block(int DF, bool LR, bool OV = false) {
+__host__ __device__ constexpr int gen_block(int DF, bool LR, int OV = 0) {
     return 64 * ((DF == 64 && !LR && !OV) ? OCX_GEN_NW64 : 4);
 }
 #ifdef OCX_GEN_TUNE_NO_STORE  // tuning only: rows computed, not written
@@ -876,8 +876,10 @@ constexpr int kRows64 = 8;
 // rounds them to float and clips them in float32 itself (algorithms.py:157-160).
 // b_off: the launch covers sequences [b_off, b_off + nseq) of the layout (a sub-batch of the
 // overlapped pipeline; 0 otherwise), a multiple of the block's waves.
-template <int MODE, int DF, bool LR = false, bool RAW = false, bool OV = false>
-__global__ __launch_bounds__(gen_block(DF, LR, OV), OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
+// OV: 0, or the overlapped form's register budget in waves per SIMD (4: 128 VGPRs, beside an
+// FTRL wave at three generator waves per SIMD; 5: 96 VGPRs, four generator waves beside one)
+template <int MODE, int DF, bool LR = false, bool RAW = false, int OV = 0>
+__global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES_FOR(DF, LR)) void ocx_gen_wave_kernel(
     uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq, int64_t T,
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
@@ -1396,6 +1398,7 @@ struct OvGeom {
     size_t lds = 0;
     int per_cu = 0;
 };
+template <int OV>
 OvGeom ov_geometry(int dev, int wps) {
     static std::mutex mu;
     static std::map<std::pair<int, int>, OvGeom> cache;
@@ -1412,7 +1415,7 @@ OvGeom ov_geometry(int dev, int wps) {
     size_t lds = base;
     int q = 0;
     for (; lds <= (size_t)lds_cu; lds += 512) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, 64, false, false, true>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, 64, false, false, OV>,
                                                          256, lds) != hipSuccess)
             break;
         if (q <= wps) break;
@@ -1436,16 +1439,26 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
     if (e != hipSuccess) return e;
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
-    const OvGeom gm = ov_geometry(dev, wps);
+    // up to three waves per SIMD the 128-VGPR form (one FTRL wave of <= 128 VGPRs fits
+    // beside it); four: the 96-VGPR form (a few spills)
+    const bool w4 = wps >= 4;
+    const OvGeom gm = w4 ? ov_geometry<5>(dev, wps) : ov_geometry<4>(dev, wps);
     const int64_t resident = (int64_t)cus * 4 * std::max(1, std::min(gm.per_cu, wps));
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const unsigned blocks = (unsigned)(((nseq + per_wave - 1) / per_wave + 3) / 4);
     const int64_t nwaves = (int64_t)blocks * 4;
-    hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, true>), dim3(blocks), dim3(256),
-                       gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d, (int)L->P,
-                       (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                       (const uint64_t*)nullptr, (uint64_t*)nullptr, ring_doubles(64, 64), nwaves,
-                       b_off);
+    if (w4)
+        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, 5>), dim3(blocks), dim3(256),
+                           gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
+                           (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
+                           (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                           ring_doubles(64, 64), nwaves, b_off);
+    else
+        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, 4>), dim3(blocks), dim3(256),
+                           gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
+                           (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
+                           (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                           ring_doubles(64, 64), nwaves, b_off);
     return hipGetLastError();
 }
 

@@ -116,17 +116,21 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     const int64_t nsub = (Bp + sub - 1) / sub;
     OCX_PIPE_TRY(ensure_events(c, (size_t)nsub));
     std::fill(c.sim_recorded.begin(), c.sim_recorded.end(), 0);
+    // tuning only (wrong outputs): time one side of the pipeline alone
+    const char* sk = std::getenv("OCX_PIPE_SKIP");
+    const bool skip_gen = sk && sk[0] == 'g', skip_sim = sk && sk[0] == 's';
     for (int64_t k = 0; k < nbatch; ++k) {
         const int64_t r0 = run0 + k * L->B;
         for (int64_t i = 0; i < nsub; ++i) {
             const int64_t b0 = i * sub, nb = std::min(sub, Bp - b0);
             // this region's previous reader (sub-batch i of batch k-1) must be done
             if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)i], 0));
-            OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st));
+            if (!skip_gen) OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st));
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], st));
             OCX_PIPE_TRY(hipStreamWaitEvent(c.sim, c.ev_gen[(size_t)i], 0));
-            OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
-                                                  cand, c.sim));
+            if (!skip_sim)
+                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
+                                                      cand, c.sim));
             const int64_t nreal = std::min(nb, L->B - b0);
             if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, c.sim));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], c.sim));

@@ -144,13 +144,13 @@ def exact_ball_solve(z, y, *, norm: str = "l2", all_prefixes: bool = True, devic
     return out
 
 
-EXACT_GAP_RTOL = 1e-6  # a general solve is accepted iff info > 0 and gap <= this * (1 + |obj|)
+EXACT_GAP_RTOL = 1e-6  # a general solve is accepted iff info >= 0 and gap <= this * (1 + |obj|)
 
 
 def check_certificates(obj, gap, info, what: str = "exact FTL") -> float:
     """The general solver's answers are only as good as their certificates
-    (include/ocx.h, ocx_exact_ball_solve): every solve must have finished (info > 0: not
-    ended by the step cap) and certify obj − optimum <= gap <= EXACT_GAP_RTOL·(1 + |obj|).
+    (include/ocx.h, ocx_exact_ball_solve): every solve must have finished (info >= 0: not
+    ended by the step cap; 0 is the empty prefix, solved without a step) and certify obj − optimum <= gap <= EXACT_GAP_RTOL·(1 + |obj|).
     A breakdown stop (OCX_EXACT_INFO_BREAKDOWN) passes only on its certificate.  Raises
     RuntimeError otherwise — what exact_ftl.py:125-126 does when cvxpy's solve fails — and
     returns the worst gap."""
@@ -159,7 +159,7 @@ def check_certificates(obj, gap, info, what: str = "exact FTL") -> float:
     info = np.asarray(info)
     if obj.size == 0:
         return 0.0
-    bad = ~((info > 0) & (gap <= EXACT_GAP_RTOL * (1.0 + np.abs(obj))))
+    bad = ~((info >= 0) & (gap <= EXACT_GAP_RTOL * (1.0 + np.abs(obj))))
     if bad.any():
         k = int(np.flatnonzero(bad.ravel())[0])
         raise RuntimeError(f"{what}: the general solver did not certify {int(bad.sum())} of "

@@ -51,7 +51,8 @@ def main():
         with open(f) as fh:
             rows += list(csv.DictReader(fh))
     # the pipelined launches: the generator's four-wave OV form and the 4-waves-per-SIMD FTRL
-    gen = intervals(rows, lambda k: "ocx_gen_wave_kernel<0, 64, false, false, true>" in k)
+    gen = intervals(rows, lambda k: "ocx_gen_wave_kernel<0, 64, false, false, 4>" in k or
+                    "ocx_gen_wave_kernel<0, 64, false, false, 5>" in k)
     ftrl = intervals(rows, lambda k: "ocx_alg_pipe_kernel" in k and k.rstrip(")").find(", 4>") >= 0)
     gu, fu = union([list(x) for x in gen]), union([list(x) for x in ftrl])
     ov = overlap(gu, fu)

@@ -33,25 +33,39 @@ def main():
     T = int(os.environ.get("OCX_PROBE_T", 10000))
     d = 64
     nb = int(os.environ.get("OCX_PROBE_NB", 4))
-    db = engine.DeviceBatch(B, T, d)
+    lanes = int(os.environ.get("OCX_PROBE_LANES", engine.LANES_BEST))
+    db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes)
     ms0, r0, g0 = run(db, nb, False)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record()
+    db.generate_gT(0, 0)
+    ev[1].record()
+    db.simulate_alg(0, math.sqrt(2))
+    ev[2].record()
+    torch.cuda.synchronize()
+    parts = {"gen_default_ms": ev[0].elapsed_time(ev[1]), "sim_default_ms": ev[1].elapsed_time(ev[2])}
     rate = lambda ms: B * T / (ms * 1e-3)
     print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
-                      "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0}), flush=True)
-    configs = [("3", "1", 0), ("3", "0", 0), ("2", "1", 0), ("3", "1", 2 * 3 * 1024),
-               ("4", "1", 0)]
+                      "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
+    configs = [("3", "0", 0), ("3", "0", 2 * 3 * 1024), ("4", "0", 0), ("3", "1", 0)]
     if os.environ.get("OCX_PROBE_CONFIGS"):
         configs = [tuple(c.split(":")[:2]) + (int(c.split(":")[2]),)
                    for c in os.environ["OCX_PROBE_CONFIGS"].split(",")]
     for wps, cand, sub in configs:
         os.environ["OCX_PIPE_WPS"] = wps
         os.environ["OCX_PIPE_CAND"] = cand
+        # each side alone (tuning knob OCX_PIPE_SKIP: outputs wrong, times only)
+        side = {}
+        for skip in ("sim", "gen"):
+            os.environ["OCX_PIPE_SKIP"] = skip
+            side["gen_only_ms" if skip == "sim" else "sim_only_ms"] = run(db, nb, True, sub)[0]
+        os.environ.pop("OCX_PIPE_SKIP")
         ms, r, g = run(db, nb, True, sub)
         print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "pipelined",
                           "wps": int(wps), "cand": cand == "1", "sub_seqs": sub,
                           "ms_per_batch": ms, "timesteps_per_s": rate(ms),
-                          "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g,
+                          "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g, **side,
                           "bitidentical": bool(np.array_equal(r, r0)) and g == g0}), flush=True)
 
 
