@@ -35,8 +35,8 @@
 // MINW: waves per SIMD the register allocation must allow (1: the whole file; 4: at most
 // 128 VGPRs, the lean form the overlapped pipeline runs beside the generator,
 // ocx_pipeline.hip).  The launch covers wave-groups [g0, g0 + gn) of the layout.
-template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1>
-__global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
+template <int C, int P, int NB, bool FTL, bool CAND>
+__device__ __forceinline__ void alg_pipe_body(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
@@ -294,6 +294,16 @@ __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
     }
 }
 
+template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1>
+__global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
+    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
+    int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
+    double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
+    int64_t gn) {
+    alg_pipe_body<C, P, NB, FTL, CAND>(zt, yt, B, T, G, eta0, regret, cum_out, comp_out,
+                                       closed_out, onepass, g0, gn);
+}
+
 namespace {
 // CAND (candidate actions formed a step early): bit-identical, and measured SLOWER on every
 // batch it was meant for (profiles/r04_pipe_probe.jsonl): 4 900 x 1e5 x 64 FTRL 40.4 ->
@@ -378,6 +388,9 @@ hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const doub
 #ifndef OCX_PIPE_LEAN_NB4
 #define OCX_PIPE_LEAN_NB4 8
 #endif
+#ifndef OCX_PIPE_LEAN168_NB
+#define OCX_PIPE_LEAN168_NB 7
+#endif
 namespace {
 template <int C, int P>
 hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, double eta0,
@@ -403,9 +416,17 @@ bool ocx_pipe_lean_supported(const ocx_layout* L) {
 
 hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
                                     double eta0, double* reg, int onepass, int64_t g0,
-                                    int64_t gn, int cand, hipStream_t st) {
+                                    int64_t gn, int cand, hipStream_t st, int vgpr_budget) {
     if (gn <= 0) return hipSuccess;
     if (g0 < 0 || g0 + gn > L->G) return hipErrorInvalidValue;
+    if (vgpr_budget >= 168 && L->P == 8 && L->C == 8 && !cand) {
+        // the 168-VGPR form (three waves per SIMD's budget) and a seven-slot ring: beside
+        // three generator waves of the 96-VGPR form (3 x 96 + 168 <= 512)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN168_NB, false, false, 3>),
+                           ocx_grid(gn, 1), dim3(64), 0, st, zt, yt, L->B, L->T, L->G, eta0, reg,
+                           (double*)nullptr, (double*)nullptr, (int*)nullptr, onepass, g0, gn);
+        return hipGetLastError();
+    }
     if (L->P == 8 && L->C == 8)
         return launch_lean<8, 8>(L, zt, yt, eta0, reg, onepass, g0, gn, cand, st);
     if (L->P == 16 && L->C == 4)

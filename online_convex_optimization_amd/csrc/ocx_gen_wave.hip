@@ -1430,7 +1430,7 @@ OvGeom ov_geometry(int dev, int wps) {
 
 hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                    int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
-                                   hipStream_t st) {
+                                   hipStream_t st, int form96) {
     if (nseq <= 0 || L->T == 0) return hipSuccess;
     if (L->d != 64 || L->P * L->C != 64 || b_off % 4 || nseq % 4) return hipErrorInvalidValue;
     if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
@@ -1441,7 +1441,7 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
     if (e != hipSuccess) return e;
     // up to three waves per SIMD the 128-VGPR form (one FTRL wave of <= 128 VGPRs fits
     // beside it); four: the 96-VGPR form (a few spills)
-    const bool w4 = wps >= 4;
+    const bool w4 = wps >= 4 || form96;
     const OvGeom gm = w4 ? ov_geometry<5>(dev, wps) : ov_geometry<4>(dev, wps);
     const int64_t resident = (int64_t)cus * 4 * std::max(1, std::min(gm.per_cu, wps));
     const int64_t per_wave = (nseq + resident - 1) / resident;

@@ -119,18 +119,26 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     // tuning only (wrong outputs): time one side of the pipeline alone
     const char* sk = std::getenv("OCX_PIPE_SKIP");
     const bool skip_gen = sk && sk[0] == 'g', skip_sim = sk && sk[0] == 's';
+    // the FTRL side's register budget (tuning, OCX_PIPE_LEAN): 128 VGPRs beside three
+    // generator waves of the 128-VGPR form or four of the 96-VGPR one; 168 beside three of
+    // the 96-VGPR form
+    const char* lb = std::getenv("OCX_PIPE_LEAN");
+    const int sim_budget = lb ? std::atoi(lb) : 128;
+    // the generator's register form: 96 VGPRs when the FTRL side takes 168 (or at wps 4)
+    const int gen96 = sim_budget >= 168 ? 1 : 0;
     for (int64_t k = 0; k < nbatch; ++k) {
         const int64_t r0 = run0 + k * L->B;
         for (int64_t i = 0; i < nsub; ++i) {
             const int64_t b0 = i * sub, nb = std::min(sub, Bp - b0);
             // this region's previous reader (sub-batch i of batch k-1) must be done
             if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)i], 0));
-            if (!skip_gen) OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st));
+            if (!skip_gen)
+                OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st, gen96));
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], st));
             OCX_PIPE_TRY(hipStreamWaitEvent(c.sim, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
                 OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
-                                                      cand, c.sim));
+                                                      cand, c.sim, sim_budget));
             const int64_t nreal = std::min(nb, L->B - b0);
             if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, c.sim));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], c.sim));

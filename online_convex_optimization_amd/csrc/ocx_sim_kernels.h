@@ -22,14 +22,17 @@ hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const doub
 // the lean form over wave-groups [g0, g0 + gn) (<= 128 VGPRs; FTRL, 8 x 8 and 16 x 4 layouts),
 // the FTRL side of the overlapped pipeline (ocx_pipeline.hip); cand: candidate-select step
 bool ocx_pipe_lean_supported(const ocx_layout* L);
+// vgpr_budget >= 168: the 168-VGPR, seven-slot 8 x 8 form (beside three generator waves of the
+// 96-VGPR form); otherwise <= 128 VGPRs
 hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
                                     double eta0, double* reg, int onepass, int64_t g0,
-                                    int64_t gn, int cand, hipStream_t st);
+                                    int64_t gn, int cand, hipStream_t st, int vgpr_budget = 128);
 // g(T) sampler over sequences [b_off, b_off + nseq) of a d = 64 layout, at most wps waves per
 // SIMD (four-wave blocks; ocx_gen_wave.hip)
+// form96: the 96-VGPR form (spills a little; beside a 168-VGPR FTRL wave at wps 3, or at wps 4)
 hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                    int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
-                                   hipStream_t st);
+                                   hipStream_t st, int form96 = 0);
 // generation overlapped with FTRL (ocx_pipeline.hip): nbatch batches of L->B runs from run0,
 // regret = the last batch's, fold(regret_sub, n, fold_arg, stream) after every sub-batch
 bool ocx_pipeline_supported(const ocx_layout* L);

@@ -48,13 +48,16 @@ def main():
     print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
                       "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
-    configs = [("3", "0", 0), ("3", "0", 2 * 3 * 1024), ("4", "0", 0), ("3", "1", 0)]
+    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs)
+    configs = [("3", "0", 0, "128"), ("3", "0", 0, "168"), ("4", "0", 0, "128"),
+               ("3", "0", 2 * 3 * 1024, "128")]
     if os.environ.get("OCX_PROBE_CONFIGS"):
-        configs = [tuple(c.split(":")[:2]) + (int(c.split(":")[2]),)
+        configs = [(c.split(":")[0], c.split(":")[1], int(c.split(":")[2]), c.split(":")[3])
                    for c in os.environ["OCX_PROBE_CONFIGS"].split(",")]
-    for wps, cand, sub in configs:
+    for wps, cand, sub, lean in configs:
         os.environ["OCX_PIPE_WPS"] = wps
         os.environ["OCX_PIPE_CAND"] = cand
+        os.environ["OCX_PIPE_LEAN"] = lean
         # each side alone (tuning knob OCX_PIPE_SKIP: outputs wrong, times only)
         side = {}
         for skip in ("sim", "gen"):
@@ -64,6 +67,7 @@ def main():
         ms, r, g = run(db, nb, True, sub)
         print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "pipelined",
                           "wps": int(wps), "cand": cand == "1", "sub_seqs": sub,
+                          "ftrl_vgprs": int(lean),
                           "ms_per_batch": ms, "timesteps_per_s": rate(ms),
                           "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g, **side,
                           "bitidentical": bool(np.array_equal(r, r0)) and g == g0}), flush=True)
