@@ -60,12 +60,21 @@ constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 #ifndef OCX_GEN_KI_DOUBLE
 #define OCX_GEN_KI_DOUBLE 1
 #endif
+// Copies of the {ki, wi} table in the d = 64 (KD) kernels.  A ds_read_b128 of a random layer
+// lands on slot idx mod 16 of the 256-B bank row, so a 16-lane group of random layers has
+// ~3 lanes on its busiest slot.  With K copies entry (idx, c) lives at idx·K + c and lane l
+// reads copy c = l mod K: each b128 group holds every c twice (its lanes mod 8 are 0..7
+// twice), so at K = 8 a group's busiest slot holds 2 lanes.  1 = a single table.
+#ifndef OCX_GEN_KW_COPIES
+#define OCX_GEN_KW_COPIES 1
+#endif
 template <bool KD>
 struct ZigTables {
+    static constexpr int kCopies = KD ? OCX_GEN_KW_COPIES : 1;
     struct alignas(16) Entry {
         typename std::conditional<KD, double, uint64_t>::type ki;
         double wi;
-    } kw[256];
+    } kw[256 * kCopies];
     double fi[256];
 };
 template <bool KD>
@@ -74,7 +83,9 @@ __device__ __forceinline__ void zig_lookup(const ZigTables<KD>& tb, int idx,
                                            double& wi) {
     if constexpr (KD) {
         typedef double f64x2 __attribute__((ext_vector_type(2)));
-        const f64x2 v = *reinterpret_cast<const f64x2*>(&tb.kw[idx]);
+        constexpr int K = ZigTables<KD>::kCopies;
+        const f64x2 v = *reinterpret_cast<const f64x2*>(
+            &tb.kw[K == 1 ? idx : idx * K + (int)(threadIdx.x & (K - 1))]);
         ki = v.x;
         wi = v.y;
     } else {
@@ -893,10 +904,11 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
     constexpr bool kDF = OCX_GEN_DEFER && MODE == 0 && DF == 64 && !LR && OCX_GEN_INNER;  // deferred wedges
     __shared__ ZigTables<kKD> tb;
     extern __shared__ double rings[];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        tb.kw[i].ki = (decltype(tb.kw[i].ki))OCX_ZIG_KI[i];  // < 2^53: exact as a double
-        tb.kw[i].wi = __longlong_as_double((long long)OCX_ZIG_WI_BITS[i]);
-        tb.fi[i] = __longlong_as_double((long long)OCX_ZIG_FI_BITS[i]);
+    for (int i = threadIdx.x; i < 256 * ZigTables<kKD>::kCopies; i += blockDim.x) {
+        const int e = i / ZigTables<kKD>::kCopies;
+        tb.kw[i].ki = (decltype(tb.kw[i].ki))OCX_ZIG_KI[e];  // < 2^53: exact as a double
+        tb.kw[i].wi = __longlong_as_double((long long)OCX_ZIG_WI_BITS[e]);
+        if (i < 256) tb.fi[i] = __longlong_as_double((long long)OCX_ZIG_FI_BITS[i]);
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;

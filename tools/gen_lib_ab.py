@@ -1,4 +1,4 @@
-"""Generator A/B (round 3) between tune_r03 libraries named on the command line, the first
+"""Generator A/B between the tuning libraries (OCX_TUNE_DIR, default tune_r04) named on the command line, the first
 the reference: checks their outputs agree (wrapping int64 sums of z and y, full and strided)
 on three shapes, then times ocx_dev_gen_gT for each (min over rounds, HIP events).
     python tools/gen_lib_ab.py rej0,rej1"""
@@ -15,7 +15,7 @@ from online_convex_optimization_amd import _lib, engine  # noqa: E402
 
 
 def lib(name):
-    L = ctypes.CDLL(os.path.join(ROOT, "tune_r03", f"libocx_{name}.so"))
+    L = ctypes.CDLL(os.path.join(ROOT, os.environ.get("OCX_TUNE_DIR", "tune_r04"), f"libocx_{name}.so"))
     L.ocx_dev_gen_gT.argtypes = _lib.SIGNATURES["ocx_dev_gen_gT"][1]
     return L
 
