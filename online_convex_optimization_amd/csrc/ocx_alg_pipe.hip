@@ -29,6 +29,13 @@
 #include <cstdlib>
 
 #include "ocx_device_math.h"
+// tuning switches (A/B through _build.build_variant; bit-identical either way)
+#ifndef OCX_PIPE_Y_SADDR
+#define OCX_PIPE_Y_SADDR 0
+#endif
+#ifndef OCX_PIPE_FTL_NOBRANCH
+#define OCX_PIPE_FTL_NOBRANCH 0
+#endif
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
@@ -85,7 +92,11 @@ __device__ __forceinline__ void alg_pipe_body(
             zb[slot][k] = row[k * kst + lane];
 #endif
         }
+#if OCX_PIPE_Y_SADDR
+        yb[slot] = (yg + tl * S)[s];  // uniform row base (SGPRs) + the lane's constant offset
+#else
         yb[slot] = yg[tl * S + s];
+#endif
     };
     double cum = 0.0;
     double scv = 0.0;  // −η0/√(t+1+lane) for the 64 steps from the last multiple of 64
@@ -227,7 +238,15 @@ __device__ __forceinline__ void alg_pipe_body(
                 tth = ocx_lane_sum<C>(p);
                 n_raw = ocx_seq_sum<P>(tth);
             }
+#if OCX_PIPE_FTL_NOBRANCH
+            // the sqrt and division on every lane (no exec-mask branch around them); where
+            // θ_t = 0 they run on 1.0 and the select keeps the reference's 0
+            const double ns = n_raw > 0.0 ? n_raw : 1.0;
+            const double rs = -(1.0 / sqrt(ns));
+            q = n_raw == 0.0 ? 0.0 : rs * q_raw;
+#else
             q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
+#endif
         }
         const double yv = yb[u];
         const double diff = q - yv;  // :106-111

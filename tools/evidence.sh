@@ -16,6 +16,7 @@
 #   genlds       LDS counters of the generator (instructions, bank conflicts, active cycles)
 #   genab        generator A/B over tuning builds (GENAB=kw1,kw8: tools/gen_lib_ab.py)
 #   genldsab     LDS counters of each tuning build (GENAB_LDS="kw1 kw8", OCX_LIB)
+#   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=p0,pys,...: tools/pipe_lib_ab.py)
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
@@ -63,6 +64,9 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && OCX_LIB="$R/tune_r04/libocx_$v.so" timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES --output-format csv -d "${O}_genlds_$v" -o lds -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_genlds_$v.log" 2>&1) || fail "genlds $v" $?
       python tools/pmc_summary.py --kernel gen_wave "${O}_genlds_$v"
     done ;;
+  pipeab)
+    timeout -k 10 500 python -u tools/pipe_lib_ab.py "${PIPEAB:-p0,pys,pftl,pboth}" > "${O}_pipeab.jsonl" 2> "${O}_pipeab.err" || fail pipeab $?
+    cut -c1-200 "${O}_pipeab.jsonl" ;;
   overlap)
     timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?
     cut -c1-260 "${O}_overlap.jsonl" ;;
