@@ -14,9 +14,9 @@
 #                tools/pmc_traffic.py (gfx950 x2 read correction) into TAG_traffic.json
 #   gensq        SQ counters of the generator (one 32 768 x 1e4 x 64 launch after a warm-up)
 #   genlds       LDS counters of the generator (instructions, bank conflicts, active cycles)
-#   genab        generator A/B over tuning builds (GENAB=kw1,kw8: tools/gen_lib_ab.py)
-#   genldsab     LDS counters of each tuning build (GENAB_LDS="kw1 kw8", OCX_LIB)
-#   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=p0,pys,...: tools/pipe_lib_ab.py)
+#   genab        generator A/B over tuning builds (GENAB=main,kw8: tools/gen_lib_ab.py)
+#   genldsab     LDS counters of each tuning build (GENAB_LDS="main kw8", OCX_LIB)
+#   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=main,pys,...: tools/pipe_lib_ab.py)
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
@@ -57,15 +57,15 @@ for step in "$@"; do
     python tools/pmc_summary.py --kernel gen_wave "${O}_genlds" ;;
   genab)
     # tuning builds tune_r04/libocx_{kw1,kw8}.so (_build.build_variant): bit identity + time
-    timeout -k 10 500 python -u tools/gen_lib_ab.py "${GENAB:-kw1,kw8}" > "${O}_genab.jsonl" 2> "${O}_genab.err" || fail genab $?
+    timeout -k 10 500 python -u tools/gen_lib_ab.py "${GENAB:-main,kw8}" > "${O}_genab.jsonl" 2> "${O}_genab.err" || fail genab $?
     cut -c1-200 "${O}_genab.jsonl" ;;
   genldsab)
-    for v in ${GENAB_LDS:-kw1 kw8}; do
-      (cd /tmp && export TMPDIR=/tmp && OCX_LIB="$R/tune_r04/libocx_$v.so" timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES --output-format csv -d "${O}_genlds_$v" -o lds -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_genlds_$v.log" 2>&1) || fail "genlds $v" $?
+    for v in ${GENAB_LDS:-main kw8}; do
+      (cd /tmp && export TMPDIR=/tmp && OCX_LIB="$( [ "$v" = main ] && echo "$R/online_convex_optimization_amd/libocx.so" || echo "$R/tune_r04/libocx_$v.so" )" timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES --output-format csv -d "${O}_genlds_$v" -o lds -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_genlds_$v.log" 2>&1) || fail "genlds $v" $?
       python tools/pmc_summary.py --kernel gen_wave "${O}_genlds_$v"
     done ;;
   pipeab)
-    timeout -k 10 500 python -u tools/pipe_lib_ab.py "${PIPEAB:-p0,pys,pftl,pboth}" > "${O}_pipeab.jsonl" 2> "${O}_pipeab.err" || fail pipeab $?
+    timeout -k 10 500 python -u tools/pipe_lib_ab.py "${PIPEAB:-main,pys,pftl}" > "${O}_pipeab.jsonl" 2> "${O}_pipeab.err" || fail pipeab $?
     cut -c1-200 "${O}_pipeab.jsonl" ;;
   overlap)
     timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?

@@ -15,7 +15,10 @@ from online_convex_optimization_amd import _lib, engine  # noqa: E402
 
 
 def lib(name):
-    L = ctypes.CDLL(os.path.join(ROOT, os.environ.get("OCX_TUNE_DIR", "tune_r04"), f"libocx_{name}.so"))
+    # "main": the product library itself (the reference of the comparison)
+    path = (os.path.join(ROOT, "online_convex_optimization_amd", "libocx.so") if name == "main" else
+            os.path.join(ROOT, os.environ.get("OCX_TUNE_DIR", "tune_r04"), f"libocx_{name}.so"))
+    L = ctypes.CDLL(path)
     L.ocx_dev_gen_gT.argtypes = _lib.SIGNATURES["ocx_dev_gen_gT"][1]
     return L
 
