@@ -81,3 +81,26 @@ def test_poly_regime_flags():
     assert not O.ftl_exact_poly(z, y, "linf")[3]    # sum |z_j| > 1 for clipped rows
     assert O.ftl_exact_poly(z / 3.0, y, "linf")[3]
     assert not O.ftl_exact_poly(z / 3.0, 0.5 * y, "linf")[3]
+
+
+def test_rows_of_gathers_sequences_out_of_the_tile():
+    """DeviceBatch.rows_of (the general solver's input for the sequences outside the regime,
+    engine.py) reads rows back out of the tiled layout (include/ocx.h ocx_layout): the same
+    rows as the row-major input, for every lane split.  CPU tensors stand in for HBM."""
+    import types
+
+    import torch
+
+    from online_convex_optimization_amd import _lib, engine
+    from tests._tiles import untile_y, untile_z
+    rng = np.random.default_rng(3)
+    for B, T, d, lanes in ((13, 7, 5, 1), (10, 4, 64, 8), (9, 3, 64, 16), (5, 6, 20, 4)):
+        L = _lib.layout(B, T, d, lanes)
+        zt = rng.standard_normal(L.z_elems)
+        yt = rng.standard_normal(L.y_elems)
+        z, y = untile_z(zt, L), untile_y(yt, L)
+        fake = types.SimpleNamespace(L=L, z=torch.from_numpy(zt), y=torch.from_numpy(yt))
+        seqs = torch.tensor([B - 1, 0, B // 2], dtype=torch.int64)
+        zb, yb = engine.DeviceBatch.rows_of(fake, seqs)
+        assert np.array_equal(zb.numpy(), z[seqs.numpy()]), (B, T, d, lanes)
+        assert np.array_equal(yb.numpy(), y[seqs.numpy()]), (B, T, d, lanes)
