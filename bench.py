@@ -331,6 +331,43 @@ def main():
                        "2*(8d+8) B/timestep (with the closed-form comparator that is exactly "
                        "the pipeline's traffic: the generator's write and one FTRL read)"}
 
+    # End to end, overlapped (ocx_dev_gen_simulate): the same e2e_steps batches'
+    # worth of runs (run0 + k*B) in one call, generation of one sub-batch beside the FTRL pass
+    # over the previous one; checked bit for bit against the same call run sequentially
+    e2e_pipe = None
+    if a.e2e_steps > 0:
+        gp = torch.zeros(1, dtype=torch.float64, device=dev)
+        gs = torch.zeros(1, dtype=torch.float64, device=dev)
+        db.generate_simulate(0, run0, 1, gmax=gp)  # warm (events, streams)
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tp0 = time.perf_counter()
+        db.generate_simulate(0, run0, a.e2e_steps, gmax=gp)
+        torch.cuda.synchronize()
+        pipe_s = time.perf_counter() - tp0
+        if dist_on:
+            t = torch.tensor([pipe_s], dtype=torch.float64, device=gdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pipe_s = float(t.item())
+        reg_p = db.regret[:B].clone()
+        db.generate_simulate(0, run0, a.e2e_steps, gmax=gs, pipelined=False)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(reg_p, db.regret[:B])) and float(gp.item()) == float(gs.item())
+        rate = world * B * T * a.e2e_steps / pipe_s
+        e2e_pipe = {"timesteps_per_s": rate, "steps": a.e2e_steps,
+                    "ms_per_batch": pipe_s / a.e2e_steps * 1e3,
+                    "roofline_frac": rate / world * 2 * (8 * d + 8) / (PEAK_HBM_GBS * 1e9),
+                    "bitidentical_to_sequential": same,
+                    "note": "ocx_dev_gen_simulate: sub-batch i+1 generated while FTRL reads "
+                            "sub-batch i (second stream; generator capped at 3 waves/SIMD, "
+                            "FTRL in a 128-VGPR form); runs run0 + k*B, k < steps; regrets "
+                            "and g(T) compared with the same call run sequentially"}
+        # back to this rank's own batch (runs run0 ..) and the default's regrets, which the
+        # parity check and the gather below read
+        db.generate_gT(base_seed=0, run0=run0)
+        db.simulate_alg(0, math.sqrt(2), closed_comparator=closed)
+
     regrets = db.regret[:B].cpu().numpy()
     ranks = None
     if dist_on:
@@ -436,6 +473,7 @@ def main():
             "parity": parity,
             "two_pass": two_pass,
             "end_to_end": e2e,
+            "end_to_end_pipelined": e2e_pipe,
             "gen_seconds": gen_s,
             "gen_timesteps_per_s": B * T / gen_s,
         }
