@@ -149,3 +149,21 @@ def test_positive_double_bit_patterns_order_as_values():
     order_b = np.argsort(bits, kind="stable")
     assert np.array_equal(v[order_v], v[order_b])
     assert v[np.argmax(bits)] == v.max()
+
+
+def test_gen_simulate_rejects_bad_arguments_before_the_gpu():
+    """ocx_dev_gen_simulate checks its arguments on the host (unknown flags, NULL regret,
+    negative run0 / nbatch) and reports them through the error channel without touching a
+    device (this container has none)."""
+    import ctypes
+    lib = _lib.load()
+    L = _lib.layout(100, 10, 64, 8)
+    buf = ctypes.c_void_p(16)  # never dereferenced: the checks come first
+    cases = [(0, 1, 0x80, buf), (0, 1, 0, None), (-1, 1, 0, buf), (0, -1, 0, buf)]
+    for run0, nbatch, flags, reg in cases:
+        rc = lib.ocx_dev_gen_simulate(ctypes.byref(L), 0, run0, nbatch, buf, buf, 1.0, reg, None,
+                                      flags, 0, None)
+        assert rc == -1, (run0, nbatch, flags, reg)
+        msg = ctypes.create_string_buffer(256)
+        lib.ocx_last_error(msg, 256)
+        assert msg.value, (run0, nbatch, flags)
