@@ -201,7 +201,7 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  *     centred step produces) at the last centre, after (info & 0xFFFFF) steps — accurate to
  *     that μ only.
  * Only a converged solve is an answer by itself; for the other two the certificate decides
- * (the engine accepts a solve iff info >= 0 and gap <= 1e-6·(1 + |obj|), and raises
+ * (the engine accepts a solve iff info >= 0 and gap <= 1e-4·(1 + |obj|), and raises
  * otherwise, as exact_ftl.py:125-126 does on a solver failure).  1 <= d <=
  * OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy: unpinned (validated
  * against scipy's HiGHS LPs and by the certificate). */

@@ -459,9 +459,12 @@ hipError_t fold_max(const double* r, int64_t n, void* acc, hipStream_t st) {
 // ocx_pipeline.hip's knobs (tuning; the defaults are the measured best): generator waves per
 // SIMD beside the FTRL kernel, and the FTRL step form (candidate-select or plain)
 int pipe_wps() {
+    // 4: four generator waves per SIMD in the 96-VGPR form beside one 128-VGPR FTRL wave;
+    // 32 768 x 1e4 x 64 measured 73.0 ms per batch, vs 78.6 at 3 waves of the 128-VGPR form
+    // and 81.0 with a 168-VGPR FTRL form beside 3 (profiles/r04_overlap.jsonl)
     const char* e = std::getenv("OCX_PIPE_WPS");
-    const int v = e ? std::atoi(e) : 3;
-    return v >= 1 && v <= 8 ? v : 3;
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 1 && v <= 8 ? v : 4;
 }
 int pipe_cand_default() {
     const char* e = std::getenv("OCX_PIPE_CAND");

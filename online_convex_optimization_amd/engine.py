@@ -144,7 +144,13 @@ def exact_ball_solve(z, y, *, norm: str = "l2", all_prefixes: bool = True, devic
     return out
 
 
-EXACT_GAP_RTOL = 1e-6  # a general solve is accepted iff info >= 0 and gap <= this * (1 + |obj|)
+# A general solve is accepted iff info >= 0 and gap <= EXACT_GAP_RTOL * (1 + |obj|).  The gap
+# is a dual bound built from the barrier's multipliers; where the optimum interpolates rows
+# exactly (n > d, real-valued rows) those multipliers are only as good as the residuals at
+# μ_end = 1e-10, so the certificate stays near 1e-5 relative while the objective itself is
+# accurate to ~1e-10 (a path run on to μ = 1e-13 moves it by 3e-10).  1e-4
+# passes those and still rejects a solve the step cap or a breakdown left far from optimal.
+EXACT_GAP_RTOL = 1e-4
 
 
 def check_certificates(obj, gap, info, what: str = "exact FTL") -> float:
