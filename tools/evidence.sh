@@ -74,7 +74,7 @@ for step in "$@"; do
     timeout -k 10 400 python -u tools/r04_pipe_probe.py > "${O}_pipe.jsonl" 2> "${O}_pipe.err" || fail pipe $?
     cut -c1-200 "${O}_pipe.jsonl" ;;
   overlaptrace)
-    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=3:0:0:128 timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
+    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=4:0:0:128 timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
     cut -c1-400 "${O}_otrace.json" ;;
   sweep)

@@ -49,8 +49,7 @@ def main():
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
                       "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
     # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs)
-    configs = [("3", "0", 0, "128"), ("3", "0", 0, "168"), ("4", "0", 0, "128"),
-               ("3", "0", 2 * 3 * 1024, "128")]
+    configs = [("4", "0", 0, "128"), ("4", "0", 2 * 4 * 1024, "128"), ("3", "0", 0, "128")]
     if os.environ.get("OCX_PROBE_CONFIGS"):
         configs = [(c.split(":")[0], c.split(":")[1], int(c.split(":")[2]), c.split(":")[3])
                    for c in os.environ["OCX_PROBE_CONFIGS"].split(",")]
