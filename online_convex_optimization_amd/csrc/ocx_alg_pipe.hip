@@ -27,6 +27,7 @@
 // cancellation, re-sums ||θ_t||² directly (||θ_t||² < 0.25: early steps, returns to the
 // origin).  The comparator pass / closed form are those of ocx_alg_kernel.
 #include <cstdlib>
+#include <type_traits>
 
 #include "ocx_device_math.h"
 // tuning switches (A/B through _build.build_variant; bit-identical either way)
@@ -36,19 +37,62 @@
 #ifndef OCX_PIPE_FTL_NOBRANCH
 #define OCX_PIPE_FTL_NOBRANCH 0
 #endif
+// FTL's near-origin test decided a step early: ||θ_{t+1}||² = ||θ_t||² + g(2 z_t·θ_t + g||z_t||²)
+// >= ||θ_t||² − |z_t·θ_t| for every g in {−½, 0, ½}, so a sequence whose ||θ_t||² − |z_t·θ_t|
+// clears 0.25 (with a margin far above the running update's rounding) cannot need the
+// re-sum at t+1.  The step then tests one wave-uniform mask formed a step earlier (a scalar
+// branch off the chain) instead of an exec-mask branch on ||θ_t||² itself; lanes of a wave
+// that may need it run the per-lane test as before.  Bit-identical.
+// The step counter's type (ocx_ring_loop): int keeps the loop tests on the scalar unit; used
+// for C <= OCX_PIPE_IT32_MAXC coordinates per lane.  Measured (r04_pipe_ab.jsonl): the 16 x 4
+// few-wave batch 35.5 -> 32.4 ms with it, while the 8 x 8 kernel's loads were scheduled with
+// shallower waits and it ran 40.2 -> 42.0 ms, so 8 x 8 keeps the int64_t counter.
+#ifndef OCX_PIPE_IT32_MAXC
+#define OCX_PIPE_IT32_MAXC 4
+#endif
+#ifndef OCX_PIPE_FTL_EARLY
+#define OCX_PIPE_FTL_EARLY 0
+#endif
+// FTRL's rescale as q = a · (1 / max(s_abs, 1)) on every lane instead of an exec-mask branch
+// on s_abs > 1: where s_abs <= 1 the factor is exactly 1.0 and q = a, bit for bit.
+#ifndef OCX_PIPE_FTRL_NOBRANCH
+#define OCX_PIPE_FTRL_NOBRANCH 0
+#endif
+
+// 1/sqrt(n) for n > 0: v_rsq_f64 and two Newton steps (r <- r + r(1 - n r²)/2), within a
+// few ulp — the fast action (FQ) below, never where the reference's rounding is promised.
+__device__ __forceinline__ double ocx_rsq_nr(double n) {
+    double r = __builtin_amdgcn_rsq(n);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const double e = __builtin_fma(-n * r, r, 1.0);
+        r = __builtin_fma(0.5 * r, e, r);
+    }
+    return r;
+}
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
 // MINW: waves per SIMD the register allocation must allow (1: the whole file; 4: at most
 // 128 VGPRs, the lean form the overlapped pipeline runs beside the generator,
 // ocx_pipeline.hip).  The launch covers wave-groups [g0, g0 + gn) of the layout.
-template <int C, int P, int NB, bool FTL, bool CAND>
+// FQ (the fast action, g(T) rows only: the caller's OCX_ALG_CLIPPED_ROWS batches): the step's
+// 1/sqrt and division — ≈30 of its ≈160 VALU instructions, and most of its dependency chain —
+// become one v_rsq_f64 refined by two Newton steps, so q_t = s_t (z_t·θ_t) · min(1, rsqrt(||θ_t||²)
+// / |s_t|) (FTRL; 1/|s_t| from the same 64-step table as s_t) or −(z_t·θ_t) · rsqrt(||θ_t||²)
+// (FTL), a few ulp from the reference's fl(1/fl(sqrt(·))).  Only a sub-gradient can turn on
+// an ulp: wherever |q_t − y_t| <= 1e-12 |q_t| (an exact tie is possible there) the step
+// recomputes q_t in the reference's rounding before the hinge and the sub-gradient, so ties
+// and their g = 0 are the reference's.  The regrets are then within the butterfly layouts'
+// 1e-12 bar, not bit-identical to the exact-rounding form (FQ = false).
+template <int C, int P, int NB, bool FTL, bool CAND, bool FQ = false>
 __device__ __forceinline__ void alg_pipe_body(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
     int64_t gn) {
     static_assert(P >= 2 && NB >= 4, "butterfly layouts, a ring holding z_{t-1} .. z_{t+1}");
+    using IT = typename std::conditional<(C <= OCX_PIPE_IT32_MAXC), int, int64_t>::type;
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
@@ -100,6 +144,10 @@ __device__ __forceinline__ void alg_pipe_body(
     };
     double cum = 0.0;
     double scv = 0.0;  // −η0/√(t+1+lane) for the 64 steps from the last multiple of 64
+    double iscv = 0.0;  // FQ: 1/|scv|
+#if OCX_PIPE_FTL_EARLY
+    uint64_t near_m = ~0ULL;  // FTL: lanes whose step may need the near-origin re-sum (θ_0 = 0)
+#endif
 
     // ---- CAND: the step's action for every value g_{t-1} can take, formed a step early.
     // g is −½, 0 or +½, so z_t·θ_t = A + g·Bz and ||θ_t||² = U + g(2V + gW) have three
@@ -153,7 +201,7 @@ __device__ __forceinline__ void alg_pipe_body(
         make_cand(zb[NB - 1], 0);  // θ_0 = 0 whatever g_{-1}: every candidate is q_0
     }
 
-    if constexpr (CAND) ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+    if constexpr (CAND) ocx_ring_loop<NB, true, IT>(T, load, [&](int u, int64_t t) {
         const ocx_d2* zp1 = zb[(u + NB - 1) % NB];  // z_{t-1}
         // ---- chain: g_{t-1} → select q_t → g_t
         double q = gp > 0.0 ? qq_p : qq_m;
@@ -204,12 +252,15 @@ __device__ __forceinline__ void alg_pipe_body(
         }
         make_cand(zc, t + 1);
     });
-    else ocx_ring_loop<NB, true>(T, load, [&](int u, int64_t t) {
+    else ocx_ring_loop<NB, true, IT>(T, load, [&](int u, int64_t t) {
         // every 64 steps: the FTRL scales of the next 64 steps (one per lane, one sqrt/div
         // per lane instead of one per step) and ||θ||²'s lane part summed afresh, so the
         // running update below drifts for at most 64 steps
         if ((t & 63) == 0) {
-            if constexpr (!FTL) scv = -(eta0 / sqrt((double)(t + 1 + lane)));
+            if constexpr (!FTL) {
+                scv = -(eta0 / sqrt((double)(t + 1 + lane)));
+                if constexpr (FQ) iscv = 1.0 / fabs(scv);
+            }
             double uu = 0.0;
 #pragma unroll
             for (int j = 0; j < C; ++j) uu = __builtin_fma(th[j], th[j], uu);
@@ -228,9 +279,26 @@ __device__ __forceinline__ void alg_pipe_body(
         if constexpr (!FTL) {
             const double sc = ocx_readlane(scv, (int)(t & 63));  // −η0/√(t+1)
             const double a = sc * q_raw;
+            if constexpr (FQ) {
+                const double isc = ocx_readlane(iscv, (int)(t & 63));
+                const double r = ocx_rsq_nr(n_raw > 1e-300 ? n_raw : 1e-300);
+                q = a * fmin(r * isc, 1.0);  // exactly a where s_abs <= 1
+                if (__ballot(fabs(q - yb[u]) <= 1e-12 * fabs(q)) != 0) {  // near a tie
+                    const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+                    if (fabs(q - yb[u]) <= 1e-12 * fabs(q)) q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
+                }
+            } else {
             const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+#if OCX_PIPE_FTRL_NOBRANCH
+            q = a * (1.0 / fmax(s_abs, 1.0));
+#else
             q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
+#endif
+            }
         } else {
+#if OCX_PIPE_FTL_EARLY
+            if (near_m != 0)  // wave-uniform, formed at step t-1
+#endif
             if (n_raw < 0.25) {  // near θ = 0: re-sum directly (see above)
                 double p[C];
 #pragma unroll
@@ -238,6 +306,17 @@ __device__ __forceinline__ void alg_pipe_body(
                 tth = ocx_lane_sum<C>(p);
                 n_raw = ocx_seq_sum<P>(tth);
             }
+#if OCX_PIPE_FTL_EARLY
+            near_m = __ballot(!(n_raw - fabs(q_raw) >= 0.25 + 1e-9 * n_raw));
+#endif
+            if constexpr (FQ) {
+                const double r = ocx_rsq_nr(n_raw > 0.0 ? n_raw : 1.0);
+                q = n_raw == 0.0 ? 0.0 : -(q_raw * r);
+                if (__ballot(fabs(q - yb[u]) <= 1e-12 * fabs(q)) != 0) {  // near a tie
+                    if (fabs(q - yb[u]) <= 1e-12 * fabs(q))
+                        q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
+                }
+            } else {
 #if OCX_PIPE_FTL_NOBRANCH
             // the sqrt and division on every lane (no exec-mask branch around them); where
             // θ_t = 0 they run on 1.0 and the select keeps the reference's 0
@@ -247,6 +326,7 @@ __device__ __forceinline__ void alg_pipe_body(
 #else
             q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
 #endif
+            }
         }
         const double yv = yb[u];
         const double diff = q - yv;  // :106-111
@@ -290,7 +370,7 @@ __device__ __forceinline__ void alg_pipe_body(
     if (__ballot(!closed) != 0) {  // wave-uniform
         double xs[C];
         ocx_action_ftl<C, P, false>(th, xs, lane);
-        ocx_ring_loop<NB>(T, load, [&](int u, int64_t) {
+        ocx_ring_loop<NB, false, IT>(T, load, [&](int u, int64_t) {
             double p[C];
 #pragma unroll
             for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
@@ -313,14 +393,14 @@ __device__ __forceinline__ void alg_pipe_body(
     }
 }
 
-template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1>
+template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1, bool FQ = false>
 __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
     int64_t gn) {
-    alg_pipe_body<C, P, NB, FTL, CAND>(zt, yt, B, T, G, eta0, regret, cum_out, comp_out,
-                                       closed_out, onepass, g0, gn);
+    alg_pipe_body<C, P, NB, FTL, CAND, FQ>(zt, yt, B, T, G, eta0, regret, cum_out, comp_out,
+                                           closed_out, onepass, g0, gn);
 }
 
 namespace {
@@ -336,6 +416,16 @@ bool pipe_cand(const ocx_layout* L) {
     if (const char* e = std::getenv("OCX_PIPE_CAND")) return std::atoi(e) != 0;
     return false;
 }
+// The fast action (FQ, see alg_pipe_body) on g(T) rows (onepass: the caller's
+// OCX_ALG_CLIPPED_ROWS).  OCX_PIPE_FASTQ=0/1 overrides the default (read per launch).
+#ifndef OCX_PIPE_FASTQ_DEFAULT
+#define OCX_PIPE_FASTQ_DEFAULT 0
+#endif
+bool pipe_fastq(int onepass) {
+    if (!onepass) return false;
+    if (const char* e = std::getenv("OCX_PIPE_FASTQ")) return std::atoi(e) != 0;
+    return OCX_PIPE_FASTQ_DEFAULT != 0;
+}
 
 template <int C, int P, bool FTL, bool CAND>
 hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt, double eta0,
@@ -345,9 +435,14 @@ hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt
     // steps in flight: one slot more than the plain kernel's ring
     constexpr int NB = nb_for(C, P) + 1 < 4 ? 4 : nb_for(C, P) + 1;
     const dim3 grid = ocx_grid(L->G, ocx_block_waves(L->G)), block(64 * ocx_block_waves(L->G));
-    hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, CAND>), grid, block, 0, st, zt, yt,
-                       L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass, (int64_t)0,
-                       L->G);
+    if (!CAND && pipe_fastq(onepass))
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, false, 1, true>), grid, block, 0,
+                           st, zt, yt, L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass,
+                           (int64_t)0, L->G);
+    else
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, CAND>), grid, block, 0, st, zt, yt,
+                           L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass, (int64_t)0,
+                           L->G);
     return hipGetLastError();
 }
 
@@ -380,7 +475,8 @@ hipError_t launch_pipe_c(const ocx_layout* L, const double* zt, const double* yt
 // butterfly layouts OCX_LANES_BEST chooses (8 x 8, 16 x 4 at d = 64; 16 x 16; 32 x 32 at
 // d = 1024) and their neighbours.  Other butterfly layouts keep the plain kernel.
 bool ocx_pipe_supported(const ocx_layout* L) {
-    return !L->chain && (L->P == 8 || L->P == 16 || L->P == 32) &&
+    // T < 2^30: the step counter is a 32-bit int (ocx_ring_loop<..., int>)
+    return !L->chain && L->T < ((int64_t)1 << 30) && (L->P == 8 || L->P == 16 || L->P == 32) &&
            (L->C == 4 || L->C == 8 || L->C == 16 || L->C == 32);
 }
 
@@ -421,6 +517,10 @@ hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, 
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, true, 4>), grid, block, 0, st, zt,
                            yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr, (double*)nullptr,
                            (int*)nullptr, onepass, g0, gn);
+    else if (pipe_fastq(onepass))
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4, true>), grid, block, 0,
+                           st, zt, yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr,
+                           (double*)nullptr, (int*)nullptr, onepass, g0, gn);
     else
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4>), grid, block, 0, st, zt,
                            yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr, (double*)nullptr,
@@ -430,7 +530,7 @@ hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, 
 }  // namespace
 
 bool ocx_pipe_lean_supported(const ocx_layout* L) {
-    return !L->chain && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
+    return !L->chain && L->T < ((int64_t)1 << 30) && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
 }
 
 hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,

@@ -57,26 +57,31 @@ constexpr int nb_for(int C, int P = 1, bool deep = true) {
 // load would overwrite (ocx_alg_pipe_kernel's z_{t-1}), which otherwise makes the register
 // allocator rotate the ring with copies at the loop's back edge — and every copy of an
 // in-flight slot is a wait for its load.
-template <int NB, bool LATE = false, class Load, class Step>
-__device__ __forceinline__ void ocx_ring_loop(int64_t T, Load&& load, Step&& step) {
+// IT: the step counter's type.  int (callers that guarantee T < 2^31, checked on the host)
+// keeps the loop's bound and clamp tests on the scalar unit: the ISA has no 64-bit signed
+// scalar compare, so an int64_t counter costs two VALU compares per step whose results the
+// scalar unit then waits for.
+template <int NB, bool LATE = false, class IT = int64_t, class Load, class Step>
+__device__ __forceinline__ void ocx_ring_loop(int64_t T_arg, Load&& load, Step&& step) {
     static_assert(NB >= (LATE ? 3 : 2), "a ring with at least one step in flight");
     constexpr int BL = NB * OCX_RING_UNROLL;  // steps per loop iteration
-    if (T <= 0) return;
+    if (T_arg <= 0) return;
+    const IT T = (IT)T_arg;
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u) {
-        load(u, u < T ? (int64_t)u : T - 1);
+        load(u, (int64_t)(u < T ? (IT)u : T - 1));
         // keep the prologue's loads in slot order: the loop header merges this order with
         // the back edge's, and a slot the scheduler loaded last here would be waited for
         // as if it were the newest load on every pass (a drain once per ring cycle)
         __builtin_amdgcn_sched_barrier(0);
     }
-    for (int64_t t0 = 0; t0 < T; t0 += BL) {
+    for (IT t0 = 0; t0 < T; t0 += BL) {
 #pragma unroll
         for (int u = 0; u < BL; ++u) {
-            const int64_t tp = t0 + u + NB - 1;
-            if (!LATE) load((u + NB - 1) % NB, tp < T ? tp : T - 1);  // unconditional: above
-            if (t0 + u < T) step(u % NB, t0 + u);  // the last block may be short
-            if (LATE) load((u + NB - 1) % NB, tp < T ? tp : T - 1);
+            const IT tp = t0 + u + NB - 1;
+            if (!LATE) load((u + NB - 1) % NB, (int64_t)(tp < T ? tp : T - 1));  // unconditional: above
+            if (t0 + u < T) step(u % NB, (int64_t)(t0 + u));  // the last block may be short
+            if (LATE) load((u + NB - 1) % NB, (int64_t)(tp < T ? tp : T - 1));
         }
     }
 }

@@ -65,6 +65,11 @@ constexpr uint64_t kMask52 = 0x000fffffffffffffULL;
 // ~3 lanes on its busiest slot.  With K copies entry (idx, c) lives at idx·K + c and lane l
 // reads copy c = l mod K: each b128 group holds every c twice (its lanes mod 8 are 0..7
 // twice), so at K = 8 a group's busiest slot holds 2 lanes.  1 = a single table.
+// Measured at K = 8 (round 4; profiles/r04_gen_kw_ab.jsonl, r04_pmc_gen_lds_*.txt): bit-
+// identical, SQ_LDS_BANK_CONFLICT 7.87e9 -> 5.38e9 cycles per 32 768 x 1e4 x 64 launch
+// (2.6 -> 1.8 per LDS instruction), and the time unchanged (57.84 vs 57.99 ms): the conflicts
+// are not on the generator's critical path, which is VALU issue.  The 32 KB table costs the
+// six-wave few-stream form its occupancy (4 900 x 1e5: 89.3 -> 118.1 ms).  Off.
 #ifndef OCX_GEN_KW_COPIES
 #define OCX_GEN_KW_COPIES 1
 #endif

@@ -32,6 +32,8 @@ struct PipeCtx {
     std::mutex mu;
     bool init = false;
     hipStream_t sim = nullptr;
+    hipStream_t gen2 = nullptr, sim2 = nullptr;  // second generator / FTRL streams (knobs)
+    hipEvent_t join_gen2 = nullptr, join_sim2 = nullptr, fork = nullptr;
     std::vector<hipEvent_t> ev_gen, ev_sim;
     std::vector<char> sim_recorded;
 };
@@ -105,8 +107,30 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     std::lock_guard<std::mutex> lk(c.mu);
     if (!c.init) {
         OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.sim, hipStreamNonBlocking));
+        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.gen2, hipStreamNonBlocking));
+        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.sim2, hipStreamNonBlocking));
+        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.join_gen2, hipEventDisableTiming));
+        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.join_sim2, hipEventDisableTiming));
+        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
         c.init = true;
     }
+    // Two streams per side: consecutive sub-batches alternate between them, so one launch's
+    // last waves need not drain before the next launch's first waves start (launches on one
+    // stream are ordered).  A sub-batch is one round of generator waves, and a round whose
+    // blocks the dispatcher does not spread evenly leaves part of the chip idle until its
+    // slowest CU is done: 32 768 x 1e4 x 64, generation alone 64.1 -> 51.0 ms, the FTRL side
+    // alone 31.1 -> 25.6 ms, pipelined 72.4 -> 66.9 ms per batch (profiles/r04_overlap2.jsonl).
+    // Sub-batches write and read disjoint regions; only the gen(i) -> FTRL(i) and
+    // FTRL(i, batch k) -> gen(i, batch k+1) events order them.  OCX_PIPE_GEN_STREAMS /
+    // OCX_PIPE_SIM_STREAMS = 1 select one stream per side (tuning).
+    const char* gs_env = std::getenv("OCX_PIPE_GEN_STREAMS");
+    const char* ss_env = std::getenv("OCX_PIPE_SIM_STREAMS");
+    const int ngs = (gs_env && std::atoi(gs_env) == 1) ? 1 : 2;
+    const int nss = (ss_env && std::atoi(ss_env) == 1) ? 1 : 2;
+    // the extra streams start after the work already queued on the caller's stream
+    OCX_PIPE_TRY(hipEventRecord(c.fork, st));
+    OCX_PIPE_TRY(hipStreamWaitEvent(c.gen2, c.fork, 0));
+    OCX_PIPE_TRY(hipStreamWaitEvent(c.sim2, c.fork, 0));
     const int64_t S = L->S;
     const int64_t Bp = L->G * S;  // sequences of the layout, padding included
     // sub-batch: whole wave-groups and whole four-wave generator blocks
@@ -126,26 +150,37 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     const int sim_budget = lb ? std::atoi(lb) : 128;
     // the generator's register form: 96 VGPRs when the FTRL side takes 168 (or at wps 4)
     const int gen96 = sim_budget >= 168 ? 1 : 0;
+    int64_t j = 0;  // sub-batch launches so far (stream alternation)
     for (int64_t k = 0; k < nbatch; ++k) {
         const int64_t r0 = run0 + k * L->B;
-        for (int64_t i = 0; i < nsub; ++i) {
+        for (int64_t i = 0; i < nsub; ++i, ++j) {
             const int64_t b0 = i * sub, nb = std::min(sub, Bp - b0);
+            hipStream_t gs = (ngs == 2 && (j & 1)) ? c.gen2 : st;
+            hipStream_t ss = (nss == 2 && (j & 1)) ? c.sim2 : c.sim;
             // this region's previous reader (sub-batch i of batch k-1) must be done
-            if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)i], 0));
+            if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(gs, c.ev_sim[(size_t)i], 0));
             if (!skip_gen)
-                OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, st, gen96));
-            OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], st));
-            OCX_PIPE_TRY(hipStreamWaitEvent(c.sim, c.ev_gen[(size_t)i], 0));
+                OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, gs, gen96));
+            OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], gs));
+            OCX_PIPE_TRY(hipStreamWaitEvent(ss, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
                 OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
-                                                      cand, c.sim, sim_budget));
+                                                      cand, ss, sim_budget));
             const int64_t nreal = std::min(nb, L->B - b0);
-            if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, c.sim));
-            OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], c.sim));
+            if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, ss));
+            OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], ss));
             c.sim_recorded[(size_t)i] = 1;
         }
     }
-    // the caller's stream sees every FTRL pass and fold done (the sim stream runs in order)
-    if (nsub > 0 && nbatch > 0) OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)nsub - 1], 0));
+    // the caller's stream sees every generator launch, FTRL pass and fold done (each stream
+    // runs in order: its last event covers it)
+    if (nsub > 0 && nbatch > 0) {
+        OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
+        OCX_PIPE_TRY(hipEventRecord(c.join_sim2, c.sim2));
+        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
+        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim2, 0));
+        OCX_PIPE_TRY(hipEventRecord(c.fork, c.sim));
+        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.fork, 0));
+    }
     return hipSuccess;
 }

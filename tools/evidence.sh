@@ -17,6 +17,7 @@
 #   genab        generator A/B over tuning builds (GENAB=main,kw8: tools/gen_lib_ab.py)
 #   genldsab     LDS counters of each tuning build (GENAB_LDS="main kw8", OCX_LIB)
 #   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=main,pys,...: tools/pipe_lib_ab.py)
+#   algsq        SQ counters of the pipelined FTRL / FTL kernels (tools/alg_sq.py, few-wave batch)
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
@@ -67,6 +68,10 @@ for step in "$@"; do
   pipeab)
     timeout -k 10 500 python -u tools/pipe_lib_ab.py "${PIPEAB:-main,pys,pftl}" > "${O}_pipeab.jsonl" 2> "${O}_pipeab.err" || fail pipeab $?
     cut -c1-200 "${O}_pipeab.jsonl" ;;
+  algsq)
+    # SQ counters of the pipelined FTRL and FTL kernels on the few-wave 4 900 x 1e5 x 64 batch
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "${O}_algsq" -o sq -- python3 "$R/tools/alg_sq.py" ${ALGSQ_SHAPE:-4900 100000 64} > "${O}_algsq.log" 2>&1) || fail algsq $?
+    python tools/pmc_summary.py --kernel alg_pipe "${O}_algsq" ;;
   overlap)
     timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?
     cut -c1-260 "${O}_overlap.jsonl" ;;
@@ -74,7 +79,7 @@ for step in "$@"; do
     timeout -k 10 400 python -u tools/r04_pipe_probe.py > "${O}_pipe.jsonl" 2> "${O}_pipe.err" || fail pipe $?
     cut -c1-200 "${O}_pipe.jsonl" ;;
   overlaptrace)
-    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=4:0:0:128 timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
+    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_SIDES=0 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:0:128:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
     cut -c1-400 "${O}_otrace.json" ;;
   sweep)

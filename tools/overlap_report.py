@@ -53,7 +53,9 @@ def main():
     # the pipelined launches: the generator's four-wave OV form and the 4-waves-per-SIMD FTRL
     gen = intervals(rows, lambda k: "ocx_gen_wave_kernel<0, 64, false, false, 4>" in k or
                     "ocx_gen_wave_kernel<0, 64, false, false, 5>" in k)
-    ftrl = intervals(rows, lambda k: "ocx_alg_pipe_kernel" in k and k.rstrip(")").find(", 4>") >= 0)
+    # the lean FTRL form: MINW = 4 (template argument 6; a seventh, FQ, may follow)
+    ftrl = intervals(rows, lambda k: "ocx_alg_pipe_kernel<" in k and
+                     [x.strip() for x in k.split("<", 1)[1].split(">", 1)[0].split(",")][5:6] == ["4"])
     gu, fu = union([list(x) for x in gen]), union([list(x) for x in ftrl])
     ov = overlap(gu, fu)
     ftrl_busy = sum(e - s for s, e in fu)

@@ -1,7 +1,8 @@
 """FTRL / FTL kernel A/B between tuning builds of ocx_alg_pipe.hip (OCX_TUNE_DIR, default
-tune_r04; _build.build_variant), the first the reference: the regrets of every build must be
-bit-identical, then each build's kernel time (min over rounds, HIP events) on the few-wave
-batches and the bench batch.
+tune_r04; _build.build_variant), the first the reference: whether the regrets of every build
+are bit-identical to the first's (and the largest relative difference, for the fast-action
+builds), then each build's kernel time (min over rounds, HIP events) on the few-wave batches
+and the bench batch.  The batches are g(T) rows (OCX_ALG_CLIPPED_ROWS), as in the sweeps.
     python tools/pipe_lib_ab.py p0,pys,pftl"""
 import ctypes
 import json
@@ -45,6 +46,8 @@ def main():
                 torch.cuda.synchronize()
                 regs.append(db.regret[:B].clone())
             same = all(torch.equal(r, regs[0]) for r in regs)
+            rel = {n: float(((r - regs[0]).abs() / regs[0].abs().clamp(min=1.0)).max())
+                   for (n, _), r in zip(libs, regs)}
             for _ in range(3):
                 for n, L in libs:
                     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -58,7 +61,7 @@ def main():
                 print(json.dumps({"lib": n, "B": B, "T": T, "d": d, "layout": [db.L.P, db.L.C],
                                   "algo": "FTL" if algo else "FTRL", "kernel_ms": ms,
                                   "frac": B * T * (8 * d + 8) / (ms * 1e-3) / 8e12,
-                                  "bitidentical": same}), flush=True)
+                                  "bitidentical": same, "max_rel_vs_first": rel[n]}), flush=True)
         del db
         torch.cuda.empty_cache()
 

@@ -3,7 +3,8 @@ against the sequential gen-then-FTRL loop, on the bench's resident batch (32 768
 OCX_LANES_BEST).  One JSON line per configuration: ms per batch, timesteps/s, fraction of
 2*(8d+8) B/step, and whether the regrets and g(T) are bit-identical to the sequential path.
 Knobs per line: OCX_PIPE_WPS (generator waves per SIMD), OCX_PIPE_CAND (FTRL step form),
-sub_seqs (sequences per sub-batch; 0 = one generator round)."""
+sub_seqs (sequences per sub-batch; 0 = one generator round), OCX_PIPE_GEN_STREAMS /
+OCX_PIPE_SIM_STREAMS (sub-batches alternating over one or two streams per side)."""
 import json
 import math
 import os
@@ -48,25 +49,33 @@ def main():
     print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
                       "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
-    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs)
-    configs = [("4", "0", 0, "128"), ("4", "0", 2 * 4 * 1024, "128"), ("3", "0", 0, "128")]
+    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs,
+    # generator streams, FTRL streams)
+    configs = [("4", "0", 0, "128", "2", "2"), ("4", "0", 0, "128", "1", "1"),
+               ("3", "0", 0, "128", "2", "2"), ("3", "0", 0, "168", "2", "2"),
+               ("4", "0", 2 * 1024, "128", "2", "2")]
     if os.environ.get("OCX_PROBE_CONFIGS"):
-        configs = [(c.split(":")[0], c.split(":")[1], int(c.split(":")[2]), c.split(":")[3])
-                   for c in os.environ["OCX_PROBE_CONFIGS"].split(",")]
-    for wps, cand, sub, lean in configs:
+        configs = []
+        for c in os.environ["OCX_PROBE_CONFIGS"].split(","):
+            f = c.split(":") + ["1", "1"]
+            configs.append((f[0], f[1], int(f[2]), f[3], f[4], f[5]))
+    for wps, cand, sub, lean, gs, ss in configs:
         os.environ["OCX_PIPE_WPS"] = wps
         os.environ["OCX_PIPE_CAND"] = cand
         os.environ["OCX_PIPE_LEAN"] = lean
+        os.environ["OCX_PIPE_GEN_STREAMS"] = gs
+        os.environ["OCX_PIPE_SIM_STREAMS"] = ss
         # each side alone (tuning knob OCX_PIPE_SKIP: outputs wrong, times only)
         side = {}
-        for skip in ("sim", "gen"):
+        # OCX_PROBE_SIDES=0 (the kernel-trace step): the pipelined run alone
+        for skip in (("sim", "gen") if os.environ.get("OCX_PROBE_SIDES", "1") != "0" else ()):
             os.environ["OCX_PIPE_SKIP"] = skip
             side["gen_only_ms" if skip == "sim" else "sim_only_ms"] = run(db, nb, True, sub)[0]
-        os.environ.pop("OCX_PIPE_SKIP")
+        os.environ.pop("OCX_PIPE_SKIP", None)
         ms, r, g = run(db, nb, True, sub)
         print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "pipelined",
                           "wps": int(wps), "cand": cand == "1", "sub_seqs": sub,
-                          "ftrl_vgprs": int(lean),
+                          "ftrl_vgprs": int(lean), "gen_streams": int(gs), "sim_streams": int(ss),
                           "ms_per_batch": ms, "timesteps_per_s": rate(ms),
                           "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g, **side,
                           "bitidentical": bool(np.array_equal(r, r0)) and g == g0}), flush=True)
