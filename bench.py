@@ -327,7 +327,8 @@ def main():
                "ms_per_batch": e2e_s / a.e2e_steps * 1e3,
                "gen_kernel_ms": gen_ms, "sim_kernel_ms": sim_ms,
                "roofline_frac": rate / world * 2 * (8 * d + 8) / (PEAK_HBM_GBS * 1e9),
-               "note": "generation (ocx_dev_gen_gT) + FTRL per resident batch; frac counts "
+               "note": "generation (ocx_dev_gen_gT: generator rounds over two streams) + "
+                       "FTRL per resident batch, one after the other; frac counts "
                        "2*(8d+8) B/timestep (with the closed-form comparator that is exactly "
                        "the pipeline's traffic: the generator's write and one FTRL read)"}
 
@@ -360,9 +361,10 @@ def main():
                     "roofline_frac": rate / world * 2 * (8 * d + 8) / (PEAK_HBM_GBS * 1e9),
                     "bitidentical_to_sequential": same,
                     "note": "ocx_dev_gen_simulate: sub-batch i+1 generated while FTRL reads "
-                            "sub-batch i (second stream; generator capped at 3 waves/SIMD, "
-                            "FTRL in a 128-VGPR form); runs run0 + k*B, k < steps; regrets "
-                            "and g(T) compared with the same call run sequentially"}
+                            "sub-batch i (one generator round per sub-batch, four 96-VGPR "
+                            "generator waves and one 128-VGPR FTRL wave per SIMD, two streams "
+                            "per side); runs run0 + k*B, k < steps; regrets and g(T) compared "
+                            "with the same call run sequentially"}
         # back to this rank's own batch (runs run0 ..) and the default's regrets, which the
         # parity check and the gather below read
         db.generate_gT(base_seed=0, run0=run0)

@@ -53,6 +53,11 @@
 #ifndef OCX_PIPE_FTL_EARLY
 #define OCX_PIPE_FTL_EARLY 0
 #endif
+// FTRL: the rescale's sqrt only in waves where a sequence may need the rescale (RT, see the
+// step): 0 never, 1 where measured faster (pipe_rt), 2 in every kernel (tuning)
+#ifndef OCX_PIPE_RESCALE_TEST
+#define OCX_PIPE_RESCALE_TEST 1
+#endif
 // FTRL's rescale as q = a · (1 / max(s_abs, 1)) on every lane instead of an exec-mask branch
 // on s_abs > 1: where s_abs <= 1 the factor is exactly 1.0 and q = a, bit for bit.
 #ifndef OCX_PIPE_FTRL_NOBRANCH
@@ -85,7 +90,7 @@ __device__ __forceinline__ double ocx_rsq_nr(double n) {
 // recomputes q_t in the reference's rounding before the hinge and the sub-gradient, so ties
 // and their g = 0 are the reference's.  The regrets are then within the butterfly layouts'
 // 1e-12 bar, not bit-identical to the exact-rounding form (FQ = false).
-template <int C, int P, int NB, bool FTL, bool CAND, bool FQ = false>
+template <int C, int P, int NB, bool FTL, bool CAND, bool FQ = false, bool RT = false>
 __device__ __forceinline__ void alg_pipe_body(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
@@ -288,12 +293,20 @@ __device__ __forceinline__ void alg_pipe_body(
                     if (fabs(q - yb[u]) <= 1e-12 * fabs(q)) q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
                 }
             } else {
+            // RT: no sequence of the wave near the rescale (s²||θ||² < 1 − 1e-12, far outside
+            // the rounding of the test below): q = s·(z·θ), without the sqrt the test below
+            // needs — what the test below would give, bit for bit.  On the g(T) rows ||sθ||
+            // stays near 0.71 and the rescale is rare.
+            if (RT && __ballot(sc * sc * n_raw >= 1.0 - 1e-12) == 0) {
+                q = a;
+            } else {
             const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
 #if OCX_PIPE_FTRL_NOBRANCH
             q = a * (1.0 / fmax(s_abs, 1.0));
 #else
             q = s_abs > 1.0 ? a * (1.0 / s_abs) : a;
 #endif
+            }
             }
         } else {
 #if OCX_PIPE_FTL_EARLY
@@ -393,14 +406,21 @@ __device__ __forceinline__ void alg_pipe_body(
     }
 }
 
+// The rescale test (RT) per kernel: measured (profiles/r04_pipe_ab3.jsonl) 3 328 x 1e5 at
+// 16 x 4: 32.5 -> 28.7 ms; the pipeline's lean 8 x 8 form: 66.7 -> 64.3 ms per batch; but the
+// 8 x 8 full form (the T = 1e5 batch): 40.8 -> 43.6 ms, which keeps the sqrt.
+template <int C, int P, int MINW>
+constexpr bool pipe_rt() {
+    return OCX_PIPE_RESCALE_TEST == 2 || (OCX_PIPE_RESCALE_TEST == 1 && !(C == 8 && P == 8 && MINW == 1));
+}
 template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1, bool FQ = false>
 __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
     int64_t gn) {
-    alg_pipe_body<C, P, NB, FTL, CAND, FQ>(zt, yt, B, T, G, eta0, regret, cum_out, comp_out,
-                                           closed_out, onepass, g0, gn);
+    alg_pipe_body<C, P, NB, FTL, CAND, FQ, pipe_rt<C, P, MINW>()>(
+        zt, yt, B, T, G, eta0, regret, cum_out, comp_out, closed_out, onepass, g0, gn);
 }
 
 namespace {

@@ -53,6 +53,19 @@ hipError_t ensure_events(PipeCtx& c, size_t n) {
     return hipSuccess;
 }
 
+hipError_t pipe_init(PipeCtx& c) {  // under c.mu
+    if (c.init) return hipSuccess;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&c.sim, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&c.gen2, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&c.sim2, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&c.join_gen2, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&c.join_sim2, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming)) != hipSuccess) return e;
+    c.init = true;
+    return hipSuccess;
+}
+
 int64_t lcm64(int64_t a, int64_t b) {
     int64_t x = a, y = b;
     while (y) {
@@ -88,6 +101,39 @@ bool ocx_pipeline_worth(const ocx_layout* L, int wps) {
     return L->G * L->S >= 4 * (int64_t)cus * 4 * std::max(1, wps);
 }
 
+// Generation alone in the pipeline's geometry (ocx_launch_gen_gT for the d = 64 batches of four
+// or more generator rounds): one round of four-wave blocks per launch, four waves per SIMD
+// (the 96-VGPR form), the launches alternating between the caller's stream and a second one so
+// that no round drains before the next starts, joined back on `st`.  The normals and labels
+// are the one-launch generator's, bit for bit (the same kernel body; every wave takes one
+// stream).  32 768 x 1e4 x 64: 57.8 ms in one launch, 51.0 ms in rounds
+// (profiles/r04_overlap2.jsonl, generation alone).
+hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
+                              double* yt, hipStream_t st) {
+    constexpr int wps = 4;
+    if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    OCX_PIPE_TRY(hipGetDevice(&dev));
+    OCX_PIPE_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    PipeCtx& c = g_pipe[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    OCX_PIPE_TRY(pipe_init(c));
+    const int64_t Bp = L->G * L->S;
+    const int64_t unit = lcm64(L->S, 4);
+    int64_t sub = (int64_t)cus * 4 * wps;
+    sub = std::max(unit, (sub + unit - 1) / unit * unit);
+    OCX_PIPE_TRY(hipEventRecord(c.fork, st));
+    OCX_PIPE_TRY(hipStreamWaitEvent(c.gen2, c.fork, 0));
+    int64_t j = 0;
+    for (int64_t b0 = 0; b0 < Bp; b0 += sub, ++j)
+        OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, run0, b0, std::min(sub, Bp - b0), wps,
+                                             zt, yt, (j & 1) ? c.gen2 : st, 1));
+    OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
+    OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
+    return hipSuccess;
+}
+
 // nbatch batches of L->B runs each (runs run0 + k·B, k < nbatch) through one z/y buffer of
 // layout L; regret[] holds the last batch's regrets, dmax (nullable, device) folds the max
 // over all of them (ocx_max_fold: bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
@@ -105,15 +151,7 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     PipeCtx& c = g_pipe[dev];
     std::lock_guard<std::mutex> lk(c.mu);
-    if (!c.init) {
-        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.sim, hipStreamNonBlocking));
-        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.gen2, hipStreamNonBlocking));
-        OCX_PIPE_TRY(hipStreamCreateWithFlags(&c.sim2, hipStreamNonBlocking));
-        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.join_gen2, hipEventDisableTiming));
-        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.join_sim2, hipEventDisableTiming));
-        OCX_PIPE_TRY(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
-        c.init = true;
-    }
+    OCX_PIPE_TRY(pipe_init(c));
     // Two streams per side: consecutive sub-batches alternate between them, so one launch's
     // last waves need not drain before the next launch's first waves start (launches on one
     // stream are ordered).  A sub-batch is one round of generator waves, and a round whose

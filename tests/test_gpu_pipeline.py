@@ -63,3 +63,44 @@ def test_pipelined_exact_layout_two_pass(eng):
         assert reg[b] == O.simulate_alg(z, y, 0, SQ2), b
     ref = max(0.0, max(O.simulate_alg(*O.gT_sample(2, T, r, d), 0, SQ2) for r in range(2 * B)))
     assert float(g.item()) == ref
+
+
+@pytest.mark.parametrize("streams", ["1", "2"])
+def test_pipelined_stream_counts(eng, streams, monkeypatch):
+    """One or two streams per side (OCX_PIPE_GEN_STREAMS / OCX_PIPE_SIM_STREAMS): the sub-batches
+    only reorder, so regrets and g(T) are the sequential loop's bit for bit."""
+    import torch
+    B, T, d = 3000, 150, 64
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=8)
+    out = {}
+    for mode in (False, True):
+        if mode:
+            monkeypatch.setenv("OCX_PIPE_GEN_STREAMS", streams)
+            monkeypatch.setenv("OCX_PIPE_SIM_STREAMS", streams)
+        g = torch.zeros(1, dtype=torch.float64, device=db.device)
+        db.generate_simulate(base_seed=4, run0=1, nbatch=3, gmax=g, pipelined=mode, sub_seqs=256)
+        torch.cuda.synchronize()
+        out[mode] = (db.regret[:B].cpu().numpy().copy(), float(g.item()))
+    assert np.array_equal(out[True][0], out[False][0])
+    assert out[True][1] == out[False][1]
+
+
+def test_generation_in_rounds_is_bit_identical(eng, monkeypatch):
+    """ocx_launch_gen_gT takes generator rounds over two streams for d = 64 batches of four or
+    more rounds: the tiles equal the single launch's (OCX_GEN_ROUNDS=0) bit for bit."""
+    import torch
+    B, T, d = 16384, 40, 64
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=eng.LANES_BEST)
+    tiles = {}
+    for rounds in ("0", "1"):
+        monkeypatch.setenv("OCX_GEN_ROUNDS", rounds)
+        db.z.fill_(float("nan"))
+        db.y.fill_(float("nan"))
+        db.generate_gT(base_seed=6, run0=3)
+        torch.cuda.synchronize()
+        tiles[rounds] = (db.z.view(torch.int64).clone(), db.y.view(torch.int64).clone())
+    assert torch.equal(tiles["0"][0], tiles["1"][0]) and torch.equal(tiles["0"][1], tiles["1"][1])
+    for b in (0, 4097, B - 1):  # sequences of the first, second and last rounds vs NumPy
+        z, y = O.gT_sample(6, T, 3 + b, d)
+        zz, yy = db.rows_of(torch.tensor([b], device=db.device))
+        assert np.array_equal(zz[0].cpu().numpy(), z) and np.array_equal(yy[0].cpu().numpy(), y), b

@@ -20,6 +20,7 @@
 #   algsq        SQ counters of the pipelined FTRL / FTL kernels (tools/alg_sq.py, few-wave batch)
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
+#   overlap1e5   the same probe on the T = 1e5 batch (4 900 x 1e5 x 64), sub-batches below a round
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
 #   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
 set -u
@@ -78,6 +79,10 @@ for step in "$@"; do
   pipe)
     timeout -k 10 400 python -u tools/r04_pipe_probe.py > "${O}_pipe.jsonl" 2> "${O}_pipe.err" || fail pipe $?
     cut -c1-200 "${O}_pipe.jsonl" ;;
+  overlap1e5)
+    # the capacity-limited T = 1e5 batch (4 900 x 1e5 x 64): sub-batches smaller than a round
+    OCX_PROBE_B=4900 OCX_PROBE_T=100000 OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=${O1E5_CONFIGS:-4:0:2456:128:2:2,4:0:1232:128:2:2,4:0:0:128:2:2} timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap1e5.jsonl" 2> "${O}_overlap1e5.err" || fail overlap1e5 $?
+    cut -c1-300 "${O}_overlap1e5.jsonl" ;;
   overlaptrace)
     (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_SIDES=0 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:0:128:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?

@@ -29,7 +29,7 @@ def lib(name):
 def main():
     st = torch.cuda.current_stream()
     libs = [(n, lib(n)) for n in sys.argv[1].split(",")]
-    shapes = [(4900, 100000, 64), (3328, 100000, 64), (32768, 10000, 64)]
+    shapes = [(4900, 100000, 64), (3328, 100000, 64), (32768, 10000, 64), (2048, 10000, 1024)]
     for B, T, d in shapes:
         db = engine.DeviceBatch(B, T, d).generate_gT(base_seed=0)
         for algo in (0, 1):
