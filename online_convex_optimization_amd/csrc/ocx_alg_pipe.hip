@@ -64,6 +64,39 @@
 #define OCX_PIPE_FTRL_NOBRANCH 0
 #endif
 
+// The correctly rounded sqrt and reciprocal as the compiler expands them, without the parts
+// for extreme operands: sqrt(n) is v_rsq_f64 and the Goldschmidt iteration the compiler
+// emits, minus its scaling of n < 2^-767 and its class fix-up of 0 and inf; 1/s is v_rcp_f64,
+// two Newton steps and the remainder correction, i.e. div_scale / div_fmas / div_fixup with
+// nothing to scale or fix.  Same operations in the same order, so the same bits, for
+// 2^-500 <= n <= 2^500 (the caller checks the range for the whole wave and otherwise takes
+// sqrt() and the division).  OCX_PIPE_FAST_SQRT (tuning until measured).
+#ifndef OCX_PIPE_FAST_SQRT
+#define OCX_PIPE_FAST_SQRT 0
+#endif
+__device__ __forceinline__ double ocx_sqrt_mid(double n) {
+    const double r = __builtin_amdgcn_rsq(n);
+    double g = n * r, h = r * 0.5;
+    const double e = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, e, g);
+    h = __builtin_fma(h, e, h);
+    double d = __builtin_fma(-g, g, n);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, n);
+    return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double ocx_div_mid(double a, double b) {  // a / b, |a| = 1
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = a * r;
+    const double rem = __builtin_fma(-b, q, a);
+    return __builtin_fma(rem, r, q);
+}
+__device__ __forceinline__ bool ocx_mid_range(double n) { return n >= 0x1p-500 && n <= 0x1p500; }
+
 // 1/sqrt(n) for n > 0: v_rsq_f64 and two Newton steps (r <- r + r(1 - n r²)/2), within a
 // few ulp — the fast action (FQ) below, never where the reference's rounding is promised.
 __device__ __forceinline__ double ocx_rsq_nr(double n) {
@@ -300,7 +333,13 @@ __device__ __forceinline__ void alg_pipe_body(
             if (RT && __ballot(sc * sc * n_raw >= 1.0 - 1e-12) == 0) {
                 q = a;
             } else {
+#if OCX_PIPE_FAST_SQRT
+            double s_abs;
+            if (__ballot(!ocx_mid_range(n_raw)) == 0) s_abs = fabs(sc) * ocx_sqrt_mid(n_raw);
+            else s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+#else
             const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
+#endif
 #if OCX_PIPE_FTRL_NOBRANCH
             q = a * (1.0 / fmax(s_abs, 1.0));
 #else
@@ -336,6 +375,11 @@ __device__ __forceinline__ void alg_pipe_body(
             const double ns = n_raw > 0.0 ? n_raw : 1.0;
             const double rs = -(1.0 / sqrt(ns));
             q = n_raw == 0.0 ? 0.0 : rs * q_raw;
+#elif OCX_PIPE_FAST_SQRT
+            if (__ballot(!ocx_mid_range(n_raw) && n_raw != 0.0) == 0)
+                q = n_raw == 0.0 ? 0.0 : (-ocx_div_mid(1.0, ocx_sqrt_mid(n_raw > 0.0 ? n_raw : 1.0))) * q_raw;
+            else
+                q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
 #else
             q = n_raw == 0.0 ? 0.0 : (-(1.0 / sqrt(n_raw))) * q_raw;
 #endif

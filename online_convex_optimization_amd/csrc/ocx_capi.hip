@@ -118,6 +118,15 @@ __global__ void ocx_max_fold_kernel(const double* __restrict__ r, int64_t n,
         atomicMax(acc, (unsigned long long)__double_as_longlong(m));
 }
 
+// acc = +0.0 by a one-lane kernel: an 8-byte hipMemsetAsync captured into a HIP graph
+// replayed as 0xb8 bytes under HIP 7 (test_pipeline_captures_into_a_graph)
+__global__ void ocx_zero_u64_kernel(unsigned long long* acc) { *acc = 0ULL; }
+
+hipError_t launch_zero_u64(unsigned long long* acc, hipStream_t st) {
+    hipLaunchKernelGGL(ocx_zero_u64_kernel, dim3(1), dim3(1), 0, st, acc);
+    return hipGetLastError();
+}
+
 hipError_t launch_max_fold(const double* r, int64_t n, unsigned long long* acc, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
@@ -460,8 +469,9 @@ hipError_t fold_max(const double* r, int64_t n, void* acc, hipStream_t st) {
 // SIMD beside the FTRL kernel, and the FTRL step form (candidate-select or plain)
 int pipe_wps() {
     // 4: four generator waves per SIMD in the 96-VGPR form beside one 128-VGPR FTRL wave;
-    // 32 768 x 1e4 x 64 measured 73.0 ms per batch, vs 78.6 at 3 waves of the 128-VGPR form
-    // and 81.0 with a 168-VGPR FTRL form beside 3 (profiles/r04_overlap.jsonl)
+    // 32 768 x 1e4 x 64 with two streams per side measured 64.3-66.9 ms per batch, vs
+    // 69.6-72.9 at 3 waves of the 128-VGPR form and 69.9-73.0 with a 168-VGPR FTRL form beside
+    // 3 (profiles/r04_overlap3.jsonl, r04_overlap4.jsonl)
     const char* e = std::getenv("OCX_PIPE_WPS");
     const int v = e ? std::atoi(e) : 4;
     return v >= 1 && v <= 8 ? v : 4;
@@ -485,12 +495,14 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
     const hipStream_t st = (hipStream_t)stream;
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(gmax);
-    if (acc) OCX_HIP(hipMemsetAsync(acc, 0, 8, st));  // +0.0
+    if (acc) OCX_HIP(launch_zero_u64(acc, st));  // +0.0
     if (nbatch == 0 || L->B == 0 || L->T == 0) return OCX_OK;
     // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
     // the reference's streamed pass (the bit-exact modes)
     const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
-    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) &&
+    // A stream under HIP graph capture takes the sequential loop: the pipeline forks work to
+    // library streams, and HIP 7's capture crashed ending a capture of that.
+    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) && !ocx_stream_capturing(st) &&
         (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
                                           regret, onepass, acc ? fold_max : nullptr, acc,

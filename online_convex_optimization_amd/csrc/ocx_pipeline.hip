@@ -84,6 +84,11 @@ int64_t lcm64(int64_t a, int64_t b) {
 
 }  // namespace
 
+bool ocx_stream_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 bool ocx_pipeline_supported(const ocx_layout* L) {
     return L->d == 64 && L->P * L->C == 64 && ocx_pipe_lean_supported(L) && L->T > 0 &&
            L->T * L->d < ((int64_t)1 << 32);

@@ -104,3 +104,31 @@ def test_generation_in_rounds_is_bit_identical(eng, monkeypatch):
         z, y = O.gT_sample(6, T, 3 + b, d)
         zz, yy = db.rows_of(torch.tensor([b], device=db.device))
         assert np.array_equal(zz[0].cpu().numpy(), z) and np.array_equal(yy[0].cpu().numpy(), y), b
+
+
+def test_pipeline_captures_into_a_graph(eng):
+    """ocx_dev_gen_simulate allocates nothing and never synchronises.  Under HIP graph capture
+    it stays on the capturing stream (sequential loop: the overlapped pipeline's fork to
+    library streams crashed HIP 7's capture), so a captured graph replays it with regrets and
+    g(T) equal to the eager, overlapped call's, bit for bit."""
+    import torch
+    B, T, d = 3000, 120, 64
+    s = torch.cuda.Stream()
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=8, stream=s)
+    ge = torch.zeros(1, dtype=torch.float64, device=db.device)
+    with torch.cuda.stream(s):
+        db.generate_simulate(base_seed=7, run0=0, nbatch=2, gmax=ge, sub_seqs=512)  # eager
+    torch.cuda.synchronize()
+    ref, gref = db.regret[:B].clone(), float(ge.item())
+    gm = torch.zeros(1, dtype=torch.float64, device=db.device)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        db.generate_simulate(base_seed=7, run0=0, nbatch=2, gmax=gm, sub_seqs=512)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        db.regret.zero_()
+        gm.zero_()
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(db.regret[:B], ref) and float(gm.item()) == gref

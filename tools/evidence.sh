@@ -17,6 +17,7 @@
 #   genab        generator A/B over tuning builds (GENAB=main,kw8: tools/gen_lib_ab.py)
 #   genldsab     LDS counters of each tuning build (GENAB_LDS="main kw8", OCX_LIB)
 #   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=main,pys,...: tools/pipe_lib_ab.py)
+#   alg          FTRL / FTL kernel times on the resident batches (tools/alg_probe.py)
 #   algsq        SQ counters of the pipelined FTRL / FTL kernels (tools/alg_sq.py, few-wave batch)
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
@@ -69,6 +70,11 @@ for step in "$@"; do
   pipeab)
     timeout -k 10 500 python -u tools/pipe_lib_ab.py "${PIPEAB:-main,pys,pftl}" > "${O}_pipeab.jsonl" 2> "${O}_pipeab.err" || fail pipeab $?
     cut -c1-200 "${O}_pipeab.jsonl" ;;
+  alg)
+    # FTRL / FTL kernel times on the resident batches (tools/alg_probe.py; ALG_SHORT=1: the
+    # few-wave d = 64 ones)
+    OCX_PROBE_SHORT=${ALG_SHORT:-} timeout -k 10 400 python -u tools/alg_probe.py > "${O}_alg.jsonl" 2> "${O}_alg.err" || fail alg $?
+    cut -c1-200 "${O}_alg.jsonl" ;;
   algsq)
     # SQ counters of the pipelined FTRL and FTL kernels on the few-wave 4 900 x 1e5 x 64 batch
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "${O}_algsq" -o sq -- python3 "$R/tools/alg_sq.py" ${ALGSQ_SHAPE:-4900 100000 64} > "${O}_algsq.log" 2>&1) || fail algsq $?
