@@ -23,6 +23,7 @@
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
 #   overlap1e5   the same probe on the T = 1e5 batch (4 900 x 1e5 x 64), sub-batches below a round
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
+#   config3      tools/perf_extra.py config3 (configs[2]: FTRL vs exact FTL, generation included)
 #   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -50,7 +51,7 @@ for step in "$@"; do
     for C in FETCH_SIZE WRITE_SIZE; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d "${O}_pmc_$C" -o pmc -- python3 "$R/bench.py" --steps 2 --warmup 0 --cpu-seconds 0 --two-pass-steps 0 --e2e-steps 1 > "${O}_pmc_$C.log" 2>&1) || fail "pmc $C" $?
     done
-    python tools/pmc_traffic.py --fetch "${O}_pmc_FETCH_SIZE" --write "${O}_pmc_WRITE_SIZE" --kernel ocx_alg_pipe_kernel --B 32768 --T 10000 --d 64 --P 8 --passes 1 --out "${O}_traffic.json" > /dev/null || fail traffic $?
+    python tools/pmc_traffic.py --fetch "${O}_pmc_FETCH_SIZE" --write "${O}_pmc_WRITE_SIZE" --kernel "ocx_alg_pipe_kernel<8, 8, 9," --label ocx_alg_pipe_kernel --B 32768 --T 10000 --d 64 --P 8 --passes 1 --out "${O}_traffic.json" > /dev/null || fail traffic $?
     head -c 600 "${O}_traffic.json"; echo ;;
   gensq)
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT --output-format csv -d "${O}_gensq" -o sq -- python3 "$R/tools/gen_only.py" 32768 10000 64 2 128 > "${O}_gensq.log" 2>&1) || fail gensq $?
@@ -93,6 +94,10 @@ for step in "$@"; do
     (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_SIDES=0 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:0:128:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
     cut -c1-400 "${O}_otrace.json" ;;
+  config3)
+    # configs[2]: FTRL vs exact FTL, 1e5 trials x 1e4 x 64, generation included
+    timeout -k 10 600 python tools/perf_extra.py config3 > "${O}_config3.log" 2>&1 || fail config3 $?
+    grep '^{' "${O}_config3.log" | cut -c1-220 ;;
   sweep)
     timeout -k 10 900 python tools/perf_extra.py sweep config4 > "${O}_sweep.log" 2>&1 || fail sweep $?
     grep '^{' "${O}_sweep.log" | cut -c1-220 ;;

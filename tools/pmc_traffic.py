@@ -44,7 +44,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
-    ap.add_argument("--kernel", default="ocx_alg_kernel")
+    ap.add_argument("--kernel", default="ocx_alg_kernel",
+                    help="substring of the kernel's name the dispatches must contain")
+    ap.add_argument("--label", default=None,
+                    help="kernel name recorded in the output (default: --kernel); bench.py "
+                         "matches it against the kernel family its layout runs")
     ap.add_argument("--B", type=int, required=True)
     ap.add_argument("--T", type=int, required=True)
     ap.add_argument("--d", type=int, required=True)
@@ -62,7 +66,7 @@ def main():
     read_bytes = 2.0 * f_kib * 1024.0
     write_bytes = w_kib * 1024.0
     alg = a.B * a.T * a.passes * (8 * a.d + 8)
-    out = {"kernel": a.kernel, "B": a.B, "T": a.T, "d": a.d, "P": a.P,
+    out = {"kernel": a.label or a.kernel, "kernel_match": a.kernel, "B": a.B, "T": a.T, "d": a.d, "P": a.P,
            "comparator": "closed" if a.passes == 1 else "two-pass",
            "dispatches": len(fetch), "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,
            "hbm_read_bytes_per_launch": read_bytes, "hbm_write_bytes_per_launch": write_bytes,
