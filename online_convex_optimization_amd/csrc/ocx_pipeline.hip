@@ -6,12 +6,13 @@
 // 64-normal row, writing at ≈3 TB/s — and the FTRL kernel by HBM reads (one pass, 6.3–6.5
 // TB/s).  Run one after the other they take gen + FTRL (57.4 + 26.1 ms per 32 768 × 1e4 × 64
 // batch).  Here a resident batch is cut into sub-batches of sequences; sub-batch i+1 is
-// generated while the FTRL kernel reads sub-batch i on a second stream.  Two things make
+// generated while the FTRL kernel reads sub-batch i on other streams.  Three things make
 // the kernels share the CUs instead of queueing behind each other:
-//   * the generator runs in four-wave blocks whose LDS request admits at most `wps` (3)
-//     blocks per CU, i.e. 3 of its 128-VGPR waves per SIMD (ocx_launch_gen_gT_range);
+//   * the generator runs in four-wave blocks whose LDS request admits at most `wps` (4)
+//     blocks per CU, i.e. 4 of its 96-VGPR waves per SIMD (ocx_launch_gen_gT_range);
 //   * the FTRL kernel runs in its lean form (<= 128 VGPRs, ocx_launch_alg_pipe_lean), so one
-//     FTRL wave fits on every SIMD beside them whenever its sub-batch is ready.
+//     FTRL wave fits on every SIMD beside them whenever its sub-batch is ready;
+//   * consecutive sub-batches alternate between two streams per side (see below).
 // A sub-batch is one round of generator waves (one stream per wave), so no generator wave
 // idles at a sub-batch's end.  Sub-batch i of batch k+1 is generated into the region FTRL
 // read for sub-batch i of batch k, after that read (events), so consecutive batches overlap
