@@ -179,7 +179,14 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     const int64_t Bp = L->G * S;  // sequences of the layout, padding included
     // sub-batch: whole wave-groups and whole four-wave generator blocks
     const int64_t unit = lcm64(S, 4);
-    int64_t sub = sub_seqs > 0 ? sub_seqs : (int64_t)cus * 4 * std::max(1, wps);
+    // sub_seqs <= 0: `rounds` generator rounds per sub-batch.  Short horizons take up to
+    // four, so a launch holds at least ≈1 000 steps per stream's worth of rounds: the g(T)
+    // sweep at T = 100 (1e6 runs) ran 3.70e9 -> 3.98e9 timesteps/s (g(T) alone 4.23e9 ->
+    // 4.59e9) with four, T = 1e3 the same with one or four, and 16 was slower at T = 1e3
+    // (profiles/r04_sweep_subrounds.jsonl).  OCX_PIPE_SUB_ROUNDS overrides (tuning).
+    int64_t rounds = std::max<int64_t>(1, std::min<int64_t>(4, 1000 / std::max<int64_t>(L->T, 1)));
+    if (const char* e = std::getenv("OCX_PIPE_SUB_ROUNDS")) rounds = std::max<int64_t>(1, std::atoll(e));
+    int64_t sub = sub_seqs > 0 ? sub_seqs : (int64_t)cus * 4 * std::max(1, wps) * rounds;
     sub = std::max(unit, (sub + unit - 1) / unit * unit);
     const int64_t nsub = (Bp + sub - 1) / sub;
     OCX_PIPE_TRY(ensure_events(c, (size_t)nsub));
