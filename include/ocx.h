@@ -420,10 +420,13 @@ int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* str
  * `stream`; complete when the stream reaches this point.
  *   Pipelined (the default where supported: d = 64 with the 8 x 8 or 16 x 4 butterfly
  * layout, and a batch of at least four generator rounds unless sub_seqs > 0 asks for it):
- * the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator round) and sub-batch i+1 is generated while the FTRL kernel reads sub-batch i on a second
- * stream of the library's, the generator capped at three waves per SIMD and the FTRL kernel
- * in a 128-VGPR form so both stay resident (csrc/ocx_pipeline.hip); consecutive batches
- * overlap the same way.  Same kernels and arithmetic as the sequential path: the regrets are
+ * the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator round, up
+ * to four below T = 1000) and sub-batch i+1 is generated while the FTRL kernel reads
+ * sub-batch i, the sub-batches alternating over two library streams per side (forked from
+ * and joined to `stream` by events), the generator at four 96-VGPR waves per SIMD and the
+ * FTRL kernel in a 128-VGPR form so both stay resident (csrc/ocx_pipeline.hip); consecutive
+ * batches overlap the same way.  On a stream under graph capture the sequential loop runs
+ * instead.  Same kernels and arithmetic as the sequential path: the regrets are
  * bit-identical to it.
  *   OCX_GENSIM_SEQUENTIAL: generate, then simulate, batch by batch on `stream` (any layout).
  *   OCX_GENSIM_TWO_PASS: the reference's streamed comparator pass instead of the certified
