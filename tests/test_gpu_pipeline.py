@@ -24,7 +24,7 @@ def eng():
 
 
 @pytest.mark.parametrize("B,T,lanes,sub", [(3000, 300, 8, 512), (2048, 257, 16, 0),
-                                           (1000, 64, 128, 0)])
+                                           (1000, 64, 128, 0), (36000, 40, 128, 0)])
 def test_pipelined_equals_sequential(eng, B, T, lanes, sub):
     import torch
     d, nb = 64, 3
