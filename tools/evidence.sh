@@ -22,6 +22,7 @@
 #   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
 #   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
 #   overlap1e5   the same probe on the T = 1e5 batch (4 900 x 1e5 x 64), sub-batches below a round
+#   pipetraffic  FETCH_SIZE / WRITE_SIZE of the overlapped pipeline's kernels (tools/pipe_traffic.py)
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
 #   config3      tools/perf_extra.py config3 (configs[2]: FTRL vs exact FTL, generation included)
 #   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
@@ -90,6 +91,14 @@ for step in "$@"; do
     # the capacity-limited T = 1e5 batch (4 900 x 1e5 x 64): sub-batches smaller than a round
     OCX_PROBE_B=4900 OCX_PROBE_T=100000 OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=${O1E5_CONFIGS:-4:0:2456:128:2:2,4:0:1232:128:2:2,4:0:0:128:2:2} timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap1e5.jsonl" 2> "${O}_overlap1e5.err" || fail overlap1e5 $?
     cut -c1-300 "${O}_overlap1e5.jsonl" ;;
+  pipetraffic)
+    # HBM bytes of the overlapped pipeline's kernels (two PMC passes over two batches; the
+    # counters serialise the dispatches, so these runs are for bytes, not time)
+    for C in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_SEQ=0 OCX_PROBE_CONFIGS=4:0:0:128:2:2 timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "${O}_ppmc_$C" -o pmc -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_ppmc_$C.log" 2>&1) || fail "pipe pmc $C" $?
+    done
+    python tools/pipe_traffic.py "${O}_ppmc_FETCH_SIZE" "${O}_ppmc_WRITE_SIZE" > "${O}_pipetraffic.json" || fail pipetraffic $?
+    cat "${O}_pipetraffic.json" ;;
   overlaptrace)
     (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_SIDES=0 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:0:128:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?

@@ -29,6 +29,28 @@ def run(db, nb, pipelined, sub=0):
     return dt / nb * 1e3, db.regret[:db.L.B].cpu().numpy().copy(), float(g.item())
 
 
+def _configs():
+    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs,
+    # generator streams, FTRL streams)
+    configs = [("4", "0", 0, "128", "2", "2"), ("4", "0", 0, "128", "1", "1"),
+               ("3", "0", 0, "128", "2", "2"), ("3", "0", 0, "168", "2", "2"),
+               ("4", "0", 2 * 1024, "128", "2", "2")]
+    if os.environ.get("OCX_PROBE_CONFIGS"):
+        configs = []
+        for c in os.environ["OCX_PROBE_CONFIGS"].split(","):
+            f = c.split(":") + ["1", "1"]
+            configs.append((f[0], f[1], int(f[2]), f[3], f[4], f[5]))
+    return configs
+
+
+def _env(wps, cand, lean, gs, ss):
+    os.environ["OCX_PIPE_WPS"] = wps
+    os.environ["OCX_PIPE_CAND"] = cand
+    os.environ["OCX_PIPE_LEAN"] = lean
+    os.environ["OCX_PIPE_GEN_STREAMS"] = gs
+    os.environ["OCX_PIPE_SIM_STREAMS"] = ss
+
+
 def main():
     B = int(os.environ.get("OCX_PROBE_B", 32768))
     T = int(os.environ.get("OCX_PROBE_T", 10000))
@@ -36,6 +58,15 @@ def main():
     nb = int(os.environ.get("OCX_PROBE_NB", 4))
     lanes = int(os.environ.get("OCX_PROBE_LANES", engine.LANES_BEST))
     db = engine.DeviceBatch(B, T, d, lanes_per_seq=lanes)
+    # OCX_PROBE_SEQ=0 (the PMC traffic step): the pipelined runs alone
+    seq = os.environ.get("OCX_PROBE_SEQ", "1") != "0"
+    configs = _configs()
+    if not seq:
+        for wps, cand, sub, lean, gs, ss in configs:
+            _env(wps, cand, lean, gs, ss)
+            ms, r, g = run(db, nb, True, sub)
+            print(json.dumps({"B": B, "T": T, "mode": "pipelined", "ms_per_batch": ms}), flush=True)
+        return
     ms0, r0, g0 = run(db, nb, False)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     ev[0].record()
@@ -49,22 +80,8 @@ def main():
     print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
                       "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
-    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs,
-    # generator streams, FTRL streams)
-    configs = [("4", "0", 0, "128", "2", "2"), ("4", "0", 0, "128", "1", "1"),
-               ("3", "0", 0, "128", "2", "2"), ("3", "0", 0, "168", "2", "2"),
-               ("4", "0", 2 * 1024, "128", "2", "2")]
-    if os.environ.get("OCX_PROBE_CONFIGS"):
-        configs = []
-        for c in os.environ["OCX_PROBE_CONFIGS"].split(","):
-            f = c.split(":") + ["1", "1"]
-            configs.append((f[0], f[1], int(f[2]), f[3], f[4], f[5]))
     for wps, cand, sub, lean, gs, ss in configs:
-        os.environ["OCX_PIPE_WPS"] = wps
-        os.environ["OCX_PIPE_CAND"] = cand
-        os.environ["OCX_PIPE_LEAN"] = lean
-        os.environ["OCX_PIPE_GEN_STREAMS"] = gs
-        os.environ["OCX_PIPE_SIM_STREAMS"] = ss
+        _env(wps, cand, lean, gs, ss)
         # each side alone (tuning knob OCX_PIPE_SKIP: outputs wrong, times only)
         side = {}
         # OCX_PROBE_SIDES=0 (the kernel-trace step): the pipelined run alone
