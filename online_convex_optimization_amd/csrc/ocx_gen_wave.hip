@@ -1479,6 +1479,26 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
     return hipGetLastError();
 }
 
+// The few-stream (LR) form over sequences [b_off, b_off + nseq) of L, one wave per stream,
+// six waves per SIMD (80 VGPRs): a generator round for ocx_run_gen_rounds' tuning forms.
+hipError_t ocx_launch_gen_gT_range_lr(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                      int64_t b_off, int64_t nseq, double* zt, double* ytl,
+                                      hipStream_t st) {
+    if (nseq <= 0 || L->T == 0) return hipSuccess;
+    if (L->d != 64 || L->P * L->C != 64 || b_off % 4 || nseq % 4) return hipErrorInvalidValue;
+    if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    constexpr int kBlock = gen_block(64, true);
+    const int rb = ring_doubles(64, 64, true);
+    const size_t lds = (size_t)rb * 8 * (kBlock / 64);
+    const unsigned blocks = (unsigned)(nseq / (kBlock / 64));
+    hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, true, false, 0>), dim3(blocks), dim3(kBlock), lds,
+                       st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d, (int)L->P,
+                       (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                       (const uint64_t*)nullptr, (uint64_t*)nullptr, rb, (int64_t)blocks * (kBlock / 64),
+                       b_off);
+    return hipGetLastError();
+}
+
 namespace {
 
 template <int MODE>

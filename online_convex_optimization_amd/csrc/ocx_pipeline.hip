@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -116,7 +117,11 @@ bool ocx_pipeline_worth(const ocx_layout* L, int wps) {
 // (profiles/r04_overlap2.jsonl, generation alone).
 hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                               double* yt, hipStream_t st) {
-    constexpr int wps = 4;
+    // OCX_GEN_ROUNDS_FORM (tuning): "ov4" (default) the 96-VGPR four-wave-block form at four
+    // waves per SIMD; "ov5" the same at five; "lr6" the few-stream form at six
+    const char* fe = std::getenv("OCX_GEN_ROUNDS_FORM");
+    const bool lr6 = fe && std::strcmp(fe, "lr6") == 0;
+    const int wps = (fe && std::strcmp(fe, "ov5") == 0) ? 5 : (lr6 ? 6 : 4);
     if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
     int dev = 0, cus = 256;
     OCX_PIPE_TRY(hipGetDevice(&dev));
@@ -133,8 +138,10 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
     OCX_PIPE_TRY(hipStreamWaitEvent(c.gen2, c.fork, 0));
     int64_t j = 0;
     for (int64_t b0 = 0; b0 < Bp; b0 += sub, ++j)
-        OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, run0, b0, std::min(sub, Bp - b0), wps,
-                                             zt, yt, (j & 1) ? c.gen2 : st, 1));
+        OCX_PIPE_TRY(lr6 ? ocx_launch_gen_gT_range_lr(L, base_seed, run0, b0, std::min(sub, Bp - b0),
+                                                      zt, yt, (j & 1) ? c.gen2 : st)
+                         : ocx_launch_gen_gT_range(L, base_seed, run0, b0, std::min(sub, Bp - b0),
+                                                   wps, zt, yt, (j & 1) ? c.gen2 : st, 1));
     OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
     OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
     return hipSuccess;

@@ -39,6 +39,9 @@ bool ocx_pipeline_supported(const ocx_layout* L);
 bool ocx_pipeline_worth(const ocx_layout* L, int wps);
 // st is being captured into a HIP graph (the multi-stream paths then stay on st)
 bool ocx_stream_capturing(hipStream_t st);
+hipError_t ocx_launch_gen_gT_range_lr(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                      int64_t b_off, int64_t nseq, double* zt, double* ytl,
+                                      hipStream_t st);
 // generation alone in rounds over two streams (ocx_pipeline.hip)
 hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                               double* yt, hipStream_t st);
