@@ -108,19 +108,20 @@ bool ocx_pipeline_worth(const ocx_layout* L, int wps) {
     return L->G * L->S >= 4 * (int64_t)cus * 4 * std::max(1, wps);
 }
 
-// Generation alone in the pipeline's geometry (ocx_launch_gen_gT for the d = 64 batches of four
-// or more generator rounds): one round of four-wave blocks per launch, four waves per SIMD
-// (the 96-VGPR form), the launches alternating between the caller's stream and a second one so
-// that no round drains before the next starts, joined back on `st`.  The normals and labels
-// are the one-launch generator's, bit for bit (the same kernel body; every wave takes one
-// stream).  32 768 x 1e4 x 64: 57.8 ms in one launch, 51.0 ms in rounds
-// (profiles/r04_overlap2.jsonl, generation alone).
+// Generation alone in rounds (ocx_launch_gen_gT for the d = 64 batches of four or more
+// generator rounds): one round of four-wave blocks per launch, one stream per wave, the
+// launches alternating between the caller's stream and a second one so that no round drains
+// before the next starts, joined back on `st`.  The normals and labels are the one-launch
+// generator's, bit for bit (the same kernel body).
 hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                               double* yt, hipStream_t st) {
-    // OCX_GEN_ROUNDS_FORM (tuning): "ov4" (default) the 96-VGPR four-wave-block form at four
-    // waves per SIMD; "ov5" the same at five; "lr6" the few-stream form at six
+    // The round's form (OCX_GEN_ROUNDS_FORM overrides, tuning): "lr6", the default, the
+    // few-stream form (80 VGPRs) at six waves per SIMD; "ov5" / "ov4" the 96-VGPR four-wave-
+    // block form at five / four.  32 768 x 1e4 x 64: 49.7 / 50.2 / 52.3 ms, one launch 58.1
+    // ms, all bit-identical (profiles/r04_gen_rounds_forms.jsonl).  Alone, more waves per SIMD
+    // pay; beside the FTRL kernel (the pipeline) the generator keeps four.
     const char* fe = std::getenv("OCX_GEN_ROUNDS_FORM");
-    const bool lr6 = fe && std::strcmp(fe, "lr6") == 0;
+    const bool lr6 = !fe || std::strcmp(fe, "lr6") == 0;
     const int wps = (fe && std::strcmp(fe, "ov5") == 0) ? 5 : (lr6 ? 6 : 4);
     if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
     int dev = 0, cus = 256;
