@@ -34,7 +34,7 @@ struct PipeCtx {
     std::mutex mu;
     bool init = false;
     hipStream_t sim = nullptr;
-    hipStream_t gen2 = nullptr, sim2 = nullptr;  // second generator / FTRL streams (knobs)
+    hipStream_t gen2 = nullptr, sim2 = nullptr;  // the second generator / FTRL streams
     hipEvent_t join_gen2 = nullptr, join_sim2 = nullptr, fork = nullptr;
     std::vector<hipEvent_t> ev_gen, ev_sim;
     std::vector<char> sim_recorded;
@@ -99,7 +99,7 @@ bool ocx_pipeline_supported(const ocx_layout* L) {
 // Whether cutting L's batch into generator rounds of `wps` waves per SIMD pays: at least four
 // sub-batches (one round each).  A batch of a round or two (the capacity-limited T = 1e5
 // batches of ~4 900 streams) would leave the generator's last round nearly empty, and one
-// round at full occupancy (ocx_launch_gen_gT) beats two at three waves per SIMD.
+// round at full occupancy (ocx_launch_gen_gT) beats two at four waves per SIMD.
 bool ocx_pipeline_worth(const ocx_layout* L, int wps) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -151,7 +151,8 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
 // nbatch batches of L->B runs each (runs run0 + k·B, k < nbatch) through one z/y buffer of
 // layout L; regret[] holds the last batch's regrets, dmax (nullable, device) folds the max
 // over all of them (ocx_max_fold: bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
-// one generator round per sub-batch.  Returns with the work queued on `st` (joined).
+// one generator round per sub-batch (up to four below T = 1000).  Returns with the work queued
+// on `st` (joined).
 hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                      int64_t nbatch, double* zt, double* yt, double eta0,
                                      double* regret, int onepass,
