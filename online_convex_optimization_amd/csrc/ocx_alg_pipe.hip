@@ -108,6 +108,11 @@ __device__ __forceinline__ double ocx_rsq_nr(double n) {
     }
     return r;
 }
+// The sub-gradient the SPEC step assumes for step t: fast_algorithms.py:27-34 with q_t
+// strictly inside (−1, 1), i.e. sign(q − y)/2 = −sign(y)/2 (y = 0: 0, checked like the rest).
+__device__ __forceinline__ double ocx_spec_grad(double y) {
+    return y > 0.0 ? -0.5 : (y < 0.0 ? 0.5 : 0.0);
+}
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
@@ -123,7 +128,8 @@ __device__ __forceinline__ double ocx_rsq_nr(double n) {
 // recomputes q_t in the reference's rounding before the hinge and the sub-gradient, so ties
 // and their g = 0 are the reference's.  The regrets are then within the butterfly layouts'
 // 1e-12 bar, not bit-identical to the exact-rounding form (FQ = false).
-template <int C, int P, int NB, bool FTL, bool CAND, bool FQ = false, bool RT = false>
+template <int C, int P, int NB, bool FTL, bool CAND, bool FQ = false, bool RT = false,
+          bool SPEC = false>
 __device__ __forceinline__ void alg_pipe_body(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
@@ -290,7 +296,16 @@ __device__ __forceinline__ void alg_pipe_body(
         }
         make_cand(zc, t + 1);
     });
-    else ocx_ring_loop<NB, true, IT>(T, load, [&](int u, int64_t t) {
+    if constexpr (CAND) {
+        if (T > 0) {
+            ocx_d2 zl[K];
+            ocx_load_tile<C>(zl, zg + (T - 1) * tstride + lane, kst);
+#pragma unroll
+            for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, ocx_zj(zl, j), th[j]);
+        }
+    }
+    auto run_plain = [&]() {
+    ocx_ring_loop<NB, true, IT>(T, load, [&](int u, int64_t t) {
         // every 64 steps: the FTRL scales of the next 64 steps (one per lane, one sqrt/div
         // per lane instead of one per step) and ||θ||²'s lane part summed afresh, so the
         // running update below drifts for at most 64 steps
@@ -419,6 +434,131 @@ __device__ __forceinline__ void alg_pipe_body(
 #pragma unroll
         for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gp, ocx_zj(zl, j), th[j]);
     }
+    };
+
+    // ---- SPEC: the sub-gradient taken as known.  On rows in the unit ball with labels ±1
+    // (the g(T) adversary: the caller's onepass batches) |q_t| <= 1, so q_t − y_t has the
+    // sign of −y_t and g_t = −y_t/2 whatever q_t is — the `clean` condition the closed-form
+    // comparator already certifies.  θ's trajectory then does not wait for q: step t takes
+    // ĝ_{t−1} = −y_{t−1}/2 (ocx_spec_grad) from the label ring, and step t−1's q (its sqrt and
+    // division for FTL, FTRL's rare rescale), hinge loss and sub-gradient are finished in
+    // step t's block, beside step t's butterflies, instead of on a chain between the steps.
+    // Every step checks the g it computes against the ĝ it assumed; the arithmetic is the
+    // plain step's, so where every check holds the results are the plain kernel's bit for
+    // bit, and a wave where one fails runs the plain loop over again (run_plain).  The rare
+    // branches (FTL near θ = 0, FTRL's rescale) are wave-uniform and decided by masks formed
+    // a step early, at the top of the step, outside the block the scheduler interleaves.
+    auto run_spec = [&]() -> bool {
+        bool ok = true;
+        double qr_p = 0.0, nr_p = 0.0, tth_p = 0.0, qa_p = 0.0, sc_p = 0.0;
+        // the pending step before step 0: q = 0 against y = 1 (loss ½, cancelled by cum's start,
+        // sub-gradient −½ = ĝ_{-1}, which multiplies the zeroed z_{-1})
+        double y_p = 1.0;
+        yb[NB - 1] = 1.0;
+        cum = T > 0 ? -0.5 : 0.0;
+        uint64_t fix_m = 0;  // lanes whose pending step needs its rare branch
+        auto fix_pending = [&]() {  // θ = th = θ_{t-1}, the pending step's
+            if (fix_m != 0) {  // wave-uniform
+                if constexpr (FTL) {
+                    if (nr_p < 0.25) {  // the plain step's near-origin re-sum
+                        double p[C];
+#pragma unroll
+                        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
+                        tth_p = ocx_lane_sum<C>(p);
+                        nr_p = ocx_seq_sum<P>(tth_p);
+                    }
+                } else {  // the plain step's rescale
+                    const double s_abs = fabs(sc_p) * sqrt(nr_p > 0.0 ? nr_p : 0.0);
+                    if (s_abs > 1.0) qa_p = qa_p * (1.0 / s_abs);
+                }
+            }
+        };
+        auto finish_pending = [&](double gs) {  // q, hinge loss, sub-gradient check
+            double qp;
+            if constexpr (FTL) qp = nr_p == 0.0 ? 0.0 : (-(1.0 / sqrt(nr_p))) * qr_p;
+            else qp = qa_p;
+            const double diff = qp - y_p;  // :106-111
+            cum += 0.5 * fabs(diff);
+            const double gq = ocx_grad(diff);
+            ok = ok & (gq == gs);
+            clean = clean & (fabs(y_p) == 1.0) & (gq == -0.5 * y_p);
+        };
+        ocx_ring_loop<NB, true, IT>(T, load, [&](int u, int64_t t) {
+            fix_pending();
+            U = tth_p;
+            if ((t & 63) == 0) {  // as the plain step
+                if constexpr (!FTL) scv = -(eta0 / sqrt((double)(t + 1 + lane)));
+                double uu = 0.0;
+#pragma unroll
+                for (int j = 0; j < C; ++j) uu = __builtin_fma(th[j], th[j], uu);
+                U = uu;
+            }
+            // ---- one block: step t's sums (θ_t from ĝ_{t-1}) beside step t−1's finish
+            const double gs = ocx_spec_grad(yb[(u + NB - 1) % NB]);  // ĝ_{t-1}
+            const double zth = __builtin_fma(gs, Bz, A);
+            const double tth = __builtin_fma(gs, __builtin_fma(gs, W, 2.0 * V), U);
+            const ocx_d2* zp1 = zb[(u + NB - 1) % NB];
+#pragma unroll
+            for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gs, ocx_zj(zp1, j), th[j]);
+            const double q_raw = ocx_seq_sum<P>(zth);
+            const double n_raw = ocx_seq_sum<P>(tth);
+            finish_pending(gs);
+            const ocx_d2* zc = zb[u];
+            const ocx_d2* zn = zb[(u + 1) % NB];
+            double w = 0.0, an = 0.0, bn = 0.0;
+#pragma unroll
+            for (int j = 0; j < C; ++j) {
+                const double zj = ocx_zj(zc, j);
+                w = __builtin_fma(zj, zj, w);
+                an = __builtin_fma(ocx_zj(zn, j), th[j], an);
+                bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
+            }
+            clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // SPEC runs onepass only
+            V = zth;
+            W = w;
+            A = an;
+            Bz = bn;
+            qr_p = q_raw;
+            nr_p = n_raw;
+            tth_p = tth;
+            y_p = yb[u];
+            if constexpr (FTL) {
+                fix_m = __ballot(n_raw < 0.25);
+            } else {
+                sc_p = ocx_readlane(scv, (int)(t & 63));  // −η0/√(t+1)
+                qa_p = sc_p * q_raw;
+                fix_m = __ballot(sc_p * sc_p * n_raw >= 1.0 - 1e-12);  // RT's test
+            }
+        });
+        if (T > 0) {
+            fix_pending();
+            const double gs = ocx_spec_grad(y_p);  // ĝ_{T-1}
+            finish_pending(gs);
+            ocx_d2 zl[K];
+            ocx_load_tile<C>(zl, zg + (T - 1) * tstride + lane, kst);
+#pragma unroll
+            for (int j = 0; j < C; ++j) th[j] = __builtin_fma(gs, ocx_zj(zl, j), th[j]);
+        }
+        return ok;
+    };
+    if constexpr (CAND) {
+    } else if constexpr (SPEC) {
+        if (__ballot(!run_spec()) != 0) {  // wave-uniform: a check failed, start again
+#pragma unroll
+            for (int j = 0; j < C; ++j) th[j] = 0.0;
+            gp = A = Bz = U = V = W = 0.0;
+            cum = scv = iscv = 0.0;
+            clean = true;
+#pragma unroll
+            for (int k = 0; k < K; ++k) zb[NB - 1][k] = ocx_d2{0.0, 0.0};
+#if OCX_PIPE_FTL_EARLY
+            near_m = ~0ULL;
+#endif
+            run_plain();
+        }
+    } else {
+        run_plain();
+    }
 
     // ---- comparator: closed form where certified (ocx_alg_kernel onepass), else the
     // reference's second streaming pass with x* = FTL(θ_T) (fast_algorithms.py:113-114)
@@ -457,13 +597,14 @@ template <int C, int P, int MINW>
 constexpr bool pipe_rt() {
     return OCX_PIPE_RESCALE_TEST == 2 || (OCX_PIPE_RESCALE_TEST == 1 && !(C == 8 && P == 8 && MINW == 1));
 }
-template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1, bool FQ = false>
+template <int C, int P, int NB, bool FTL, bool CAND, int MINW = 1, bool FQ = false,
+          bool SPEC = false>
 __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t G, double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
     double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t g0,
     int64_t gn) {
-    alg_pipe_body<C, P, NB, FTL, CAND, FQ, pipe_rt<C, P, MINW>()>(
+    alg_pipe_body<C, P, NB, FTL, CAND, FQ, pipe_rt<C, P, MINW>(), SPEC>(
         zt, yt, B, T, G, eta0, regret, cum_out, comp_out, closed_out, onepass, g0, gn);
 }
 
@@ -490,6 +631,19 @@ bool pipe_fastq(int onepass) {
     if (const char* e = std::getenv("OCX_PIPE_FASTQ")) return std::atoi(e) != 0;
     return OCX_PIPE_FASTQ_DEFAULT != 0;
 }
+// The SPEC step (see alg_pipe_body) on onepass batches: OCX_PIPE_SPEC=0/1 overrides the
+// default per algorithm (read per launch).
+#ifndef OCX_PIPE_SPEC_FTL
+#define OCX_PIPE_SPEC_FTL 0
+#endif
+#ifndef OCX_PIPE_SPEC_FTRL
+#define OCX_PIPE_SPEC_FTRL 0
+#endif
+bool pipe_spec(int onepass, bool ftl) {
+    if (!onepass) return false;
+    if (const char* e = std::getenv("OCX_PIPE_SPEC")) return std::atoi(e) != 0;
+    return (ftl ? OCX_PIPE_SPEC_FTL : OCX_PIPE_SPEC_FTRL) != 0;
+}
 
 template <int C, int P, bool FTL, bool CAND>
 hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt, double eta0,
@@ -503,6 +657,10 @@ hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, false, 1, true>), grid, block, 0,
                            st, zt, yt, L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass,
                            (int64_t)0, L->G);
+    else if (!CAND && pipe_spec(onepass, FTL))
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, false, 1, false, true>), grid,
+                           block, 0, st, zt, yt, L->B, L->T, L->G, eta0, reg, cum, comp,
+                           closed_out, onepass, (int64_t)0, L->G);
     else
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, CAND>), grid, block, 0, st, zt, yt,
                            L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass, (int64_t)0,
@@ -584,6 +742,10 @@ hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, 
     else if (pipe_fastq(onepass))
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4, true>), grid, block, 0,
                            st, zt, yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr,
+                           (double*)nullptr, (int*)nullptr, onepass, g0, gn);
+    else if (pipe_spec(onepass, false))
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4, false, true>), grid,
+                           block, 0, st, zt, yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr,
                            (double*)nullptr, (int*)nullptr, onepass, g0, gn);
     else
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4>), grid, block, 0, st, zt,

@@ -99,3 +99,35 @@ def test_pipe_kernel_long_horizon_drift(eng):
     for b in (0, 3, 7):
         zz, yy = O.gT_sample(11, T, b, d)
         assert close(r[b], O.simulate_alg(zz, yy, 0, SQ2)), b
+
+
+@pytest.mark.parametrize("P,d", [(8, 64), (16, 64), (32, 1024)])
+def test_spec_step_is_bit_identical(eng, P, d, monkeypatch):
+    """The SPEC step (ĝ_{t-1} = −y_{t-1}/2 assumed, every step checked, a wave whose check
+    fails runs the plain loop again) against the plain pipelined step, OCX_PIPE_SPEC read per
+    launch: bit for bit on g(T) rows (no check fails) and on a batch whose checks fail in some
+    waves (a row outside the ball, labels other than ±1, exact ties on one-coordinate rows)."""
+    import torch
+    B, T = 70, 300
+    rng = np.random.default_rng(P + d)
+    z = rng.standard_normal((B, T, d))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    z[3] *= 1.7
+    y[40, ::9] = 0.5
+    zf, yf, _ = O.flip_sequence(T, d=d)
+    z[60], y[60] = zf, yf
+    batches = [eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y),
+               eng.DeviceBatch(3 * 64 // P + 5, 2000, d, lanes_per_seq=P).generate_gT(7)]
+    for db in batches:
+        for flag in (0, 1):
+            out = {}
+            for spec in ("0", "1"):
+                monkeypatch.setenv("OCX_PIPE_SPEC", spec)
+                closed = torch.zeros(db.L.B, dtype=torch.int32, device=db.device)
+                r = db.simulate_alg(flag, SQ2, closed_comparator=True, closed_out=closed)
+                torch.cuda.synchronize()
+                out[spec] = (r[:db.L.B].cpu().numpy().copy(), db.cum[:db.L.B].cpu().numpy().copy(),
+                             closed[:db.L.B].cpu().numpy().copy())
+            for a, b in zip(out["0"], out["1"]):
+                assert np.array_equal(a, b), (P, d, flag)

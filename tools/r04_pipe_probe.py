@@ -1,7 +1,8 @@
-"""Round 4: the pipelined butterfly kernel with and without the candidate-select step
-(OCX_PIPE_CAND, csrc/ocx_alg_pipe.hip) on the few-wave batches and the bench batch.  One
-JSON line per (batch, algorithm, form): kernel ms, fraction of 8 TB/s, and whether the
-regrets of the two forms are bit-identical (they must be)."""
+"""Round 4: the pipelined butterfly kernel with and without one of its step forms (the knob
+OCX_PROBE_KNOB names: OCX_PIPE_CAND, the candidate-select step, by default; OCX_PIPE_SPEC,
+the speculative sub-gradient step; csrc/ocx_alg_pipe.hip) on the few-wave batches and the
+bench batch.  One JSON line per (batch, algorithm, form): kernel ms, fraction of 8 TB/s, and
+whether the regrets of the two forms are bit-identical (they must be)."""
 import json
 import math
 import os
@@ -12,6 +13,9 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from online_convex_optimization_amd import engine  # noqa: E402
+
+
+KNOB = os.environ.get("OCX_PROBE_KNOB", "OCX_PIPE_CAND")
 
 
 def timed(db, algo, reps):
@@ -35,18 +39,18 @@ def main():
         for algo in (0, 1):
             res = {}
             for cand in ("0", "1"):
-                os.environ["OCX_PIPE_CAND"] = cand
+                os.environ[KNOB] = cand
                 res[cand] = timed(db, algo, 3)
             same = bool(np.array_equal(res["0"][1], res["1"][1]))
             for cand, (ms, _) in res.items():
                 gbs = B * T * (8 * d + 8) / (ms * 1e-3) / 1e9
                 print(json.dumps({"B": B, "T": T, "d": d, "layout": [db.L.P, db.L.C],
-                                  "algo": "FTL" if algo else "FTRL", "cand": cand == "1",
+                                  "algo": "FTL" if algo else "FTRL", "knob": KNOB, "on": cand == "1",
                                   "kernel_ms": ms, "frac": gbs / 8000.0,
                                   "bitidentical_forms": same}), flush=True)
         del db
         torch.cuda.empty_cache()
-    os.environ.pop("OCX_PIPE_CAND", None)
+    os.environ.pop(KNOB, None)
 
 
 if __name__ == "__main__":
