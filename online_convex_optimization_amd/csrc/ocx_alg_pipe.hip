@@ -632,7 +632,11 @@ bool pipe_fastq(int onepass) {
     return OCX_PIPE_FASTQ_DEFAULT != 0;
 }
 // The SPEC step (see alg_pipe_body) on onepass batches: OCX_PIPE_SPEC=0/1 overrides the
-// default per algorithm (read per launch).
+// default per algorithm (read per launch).  Measured bit-identical and no faster on the
+// few-wave batches (profiles/r04_pipe_spec_ab.jsonl: 4 900 x 1e5 x 64 FTRL 40.2 -> 42.9 ms,
+// FTL 45.9 -> 46.3), so off.  The full form only: in the pipeline's 128-VGPR lean form its
+// fallback loop spilled, and it measured no faster there either (65.9 / 65.8 vs 65.8 /
+// 65.6 ms per batch, profiles/r04_overlap_spec_ab.jsonl).
 #ifndef OCX_PIPE_SPEC_FTL
 #define OCX_PIPE_SPEC_FTL 0
 #endif
@@ -742,10 +746,6 @@ hipError_t launch_lean(const ocx_layout* L, const double* zt, const double* yt, 
     else if (pipe_fastq(onepass))
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4, true>), grid, block, 0,
                            st, zt, yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr,
-                           (double*)nullptr, (int*)nullptr, onepass, g0, gn);
-    else if (pipe_spec(onepass, false))
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4, false, true>), grid,
-                           block, 0, st, zt, yt, L->B, L->T, L->G, eta0, reg, (double*)nullptr,
                            (double*)nullptr, (int*)nullptr, onepass, g0, gn);
     else
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, false, 4>), grid, block, 0, st, zt,
