@@ -131,3 +131,28 @@ def test_spec_step_is_bit_identical(eng, P, d, monkeypatch):
                              closed[:db.L.B].cpu().numpy().copy())
             for a, b in zip(out["0"], out["1"]):
                 assert np.array_equal(a, b), (P, d, flag)
+
+
+@pytest.mark.parametrize("T", [1, 2, 64, 65])
+def test_spec_step_short_horizons(eng, T, monkeypatch):
+    """SPEC at horizons around its pending-step bookkeeping (the step before step 0, the
+    last step finished after the loop, the 64-step refresh): bit for bit with the plain step
+    and within the bar of the C oracle."""
+    import torch
+    B, d, P = 24, 64, 8
+    rng = np.random.default_rng(T)
+    z = rng.standard_normal((B, T, d))
+    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
+    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
+    db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y)
+    for flag in (0, 1):
+        ref = O.simulate_alg_batch(z, y, flag, SQ2, nthreads=4)
+        out = {}
+        for spec in ("0", "1"):
+            monkeypatch.setenv("OCX_PIPE_SPEC", spec)
+            r = db.simulate_alg(flag, SQ2, closed_comparator=True)
+            torch.cuda.synchronize()
+            out[spec] = (r[:B].cpu().numpy().copy(), db.cum[:B].cpu().numpy().copy())
+        assert np.array_equal(out["0"][0], out["1"][0]) and np.array_equal(out["0"][1], out["1"][1])
+        assert close(out["1"][1], ref[1]), (T, flag)
+        assert close_closed(out["1"][0], ref[0], T), (T, flag)
