@@ -47,6 +47,9 @@
 // for C <= OCX_PIPE_IT32_MAXC coordinates per lane.  Measured (r04_pipe_ab.jsonl): the 16 x 4
 // few-wave batch 35.5 -> 32.4 ms with it, while the 8 x 8 kernel's loads were scheduled with
 // shallower waits and it ran 40.2 -> 42.0 ms, so 8 x 8 keeps the int64_t counter.
+#ifndef OCX_PIPE_WAVE_CLOCK  // diagnostic: per-wave clocks instead of cum / comp (see below)
+#define OCX_PIPE_WAVE_CLOCK 0
+#endif
 #ifndef OCX_PIPE_IT32_MAXC
 #define OCX_PIPE_IT32_MAXC 4
 #endif
@@ -116,6 +119,20 @@ __device__ __forceinline__ double ocx_spec_grad(double y) {
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
+// Wave-group of this wave when gn groups run in blocks of W waves.  A plain blockIdx * W +
+// wave mapping leaves the nblk * W − gn spare slots in the last block, so a few-wave launch
+// ends with a block of one or two waves, alone on its CU — and a lone FTL wave measured
+// ≈10 % slower than its neighbours in full blocks, setting the launch's time
+// (profiles/r04_wave_clock*.jsonl).  Here the last `idle` blocks hold W − 1 groups each
+// instead (W = 4: at least three waves per CU); a spare slot gets gn and exits.
+__device__ __forceinline__ int64_t ocx_pipe_wave_id(int64_t gn) {
+    const int64_t W = blockDim.x >> 6, blk = blockIdx.x, w = threadIdx.x >> 6;
+    const int64_t idle = (int64_t)gridDim.x * W - gn;
+    const int64_t full = (int64_t)gridDim.x - idle;  // blocks of W groups
+    if (idle <= 0 || full < 0 || blk < full) return blk * W + w;
+    return w < W - 1 ? full * W + (blk - full) * (W - 1) + w : gn;
+}
+
 // MINW: waves per SIMD the register allocation must allow (1: the whole file; 4: at most
 // 128 VGPRs, the lean form the overlapped pipeline runs beside the generator,
 // ocx_pipeline.hip).  The launch covers wave-groups [g0, g0 + gn) of the layout.
@@ -142,15 +159,24 @@ __device__ __forceinline__ void alg_pipe_body(
     const int lane = threadIdx.x & 63;
     // wave-uniform, provably (readfirstlane): the tile bases live in SGPRs and every load
     // is an SGPR base + the lane's constant offset, with no per-load address arithmetic
-    const int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_wave_id());
+    const int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_pipe_wave_id(gn));
     if (wv >= gn) return;
     const int64_t g = g0 + wv;
+#if OCX_PIPE_WAVE_CLOCK  // diagnostic build only: see the end of the body
+    const uint64_t clk0 = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef OCX_ALG_PRIO  // tuning: issue priority over waves of a kernel running beside it
     __builtin_amdgcn_s_setprio(OCX_ALG_PRIO);
 #endif
     const int s = lane / P;
     const int c = lane % P;
     const int64_t b = g * S + s;
+    // The layout's padding sequences (b >= B, the last wave-group's spare slots) have all-zero
+    // rows, so their θ stays 0 and FTL's near-origin re-sum below would run for them at every
+    // step — in the one wave that holds them, which then set the launch's time (a 47.6 ms
+    // straggler among 41–42 ms waves on the 4 900 x 1e5 batch, profiles/r04_wave_clock*.jsonl).
+    // Their results are never written, so they skip it.
+    const bool live = b < B;
     const int64_t tstride = 64;  // ocx_d2 per step within a plane
     const ocx_d2* __restrict__ zg = reinterpret_cast<const ocx_d2*>(zt) + g * T * tstride;
     const int64_t kst = G * T * 64;  // plane stride (pairs k)
@@ -214,7 +240,7 @@ __device__ __forceinline__ void alg_pipe_body(
             const double s_abs = fabs(sc) * sqrt(n_raw > 0.0 ? n_raw : 0.0);
             return s_abs > 1.0 ? a * (1.0 / s_abs) : a;
         } else {
-            if (__ballot(n_raw < 0.25) != 0) {  // wave-uniform; per sequence below
+            if (__ballot(n_raw < 0.25 && live) != 0) {  // wave-uniform; per sequence below
                 double p[C];
 #pragma unroll
                 for (int j = 0; j < C; ++j) {
@@ -223,7 +249,7 @@ __device__ __forceinline__ void alg_pipe_body(
                 }
                 const double tld = ocx_lane_sum<C>(p);
                 const double nd = ocx_seq_sum<P>(tld);
-                if (n_raw < 0.25) {
+                if (n_raw < 0.25 && live) {
                     tl = tld;
                     n_raw = nd;
                 }
@@ -366,7 +392,7 @@ __device__ __forceinline__ void alg_pipe_body(
 #if OCX_PIPE_FTL_EARLY
             if (near_m != 0)  // wave-uniform, formed at step t-1
 #endif
-            if (n_raw < 0.25) {  // near θ = 0: re-sum directly (see above)
+            if (n_raw < 0.25 && live) {  // near θ = 0: re-sum directly (see above)
                 double p[C];
 #pragma unroll
                 for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
@@ -374,7 +400,7 @@ __device__ __forceinline__ void alg_pipe_body(
                 n_raw = ocx_seq_sum<P>(tth);
             }
 #if OCX_PIPE_FTL_EARLY
-            near_m = __ballot(!(n_raw - fabs(q_raw) >= 0.25 + 1e-9 * n_raw));
+            near_m = __ballot(live && !(n_raw - fabs(q_raw) >= 0.25 + 1e-9 * n_raw));
 #endif
             if constexpr (FQ) {
                 const double r = ocx_rsq_nr(n_raw > 0.0 ? n_raw : 1.0);
@@ -460,7 +486,7 @@ __device__ __forceinline__ void alg_pipe_body(
         auto fix_pending = [&]() {  // θ = th = θ_{t-1}, the pending step's
             if (fix_m != 0) {  // wave-uniform
                 if constexpr (FTL) {
-                    if (nr_p < 0.25) {  // the plain step's near-origin re-sum
+                    if (nr_p < 0.25 && live) {  // the plain step's near-origin re-sum
                         double p[C];
 #pragma unroll
                         for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
@@ -523,7 +549,7 @@ __device__ __forceinline__ void alg_pipe_body(
             tth_p = tth;
             y_p = yb[u];
             if constexpr (FTL) {
-                fix_m = __ballot(n_raw < 0.25);
+                fix_m = __ballot(n_raw < 0.25 && live);
             } else {
                 sc_p = ocx_readlane(scv, (int)(t & 63));  // −η0/√(t+1)
                 qa_p = sc_p * q_raw;
@@ -584,9 +610,20 @@ __device__ __forceinline__ void alg_pipe_body(
     }
     if (c == 0 && b < B) {
         if (regret) regret[b] = cum - comp;
+#if OCX_PIPE_WAVE_CLOCK
+        // diagnostic build (tools/wave_clock_probe.py): the wave's duration in ticks of the
+        // 100 MHz real-time clock, and where it ran (HW_ID, XCC_ID) — not results
+        const uint64_t clk1 = __builtin_amdgcn_s_memrealtime();
+        if (cum_out) cum_out[b] = (double)(clk1 - clk0);
+        if (comp_out) comp_out[b] = (double)clk0;
+        if (closed_out)
+            closed_out[b] = (int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xffffu) |
+                                  ((__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xfu) << 16));
+#else
         if (cum_out) cum_out[b] = cum;
         if (comp_out) comp_out[b] = comp;
         if (closed_out) closed_out[b] = closed ? 1 : 0;
+#endif
     }
 }
 
@@ -643,6 +680,15 @@ bool pipe_fastq(int onepass) {
 #ifndef OCX_PIPE_SPEC_FTRL
 #define OCX_PIPE_SPEC_FTRL 0
 #endif
+// Waves per block of the full-form launch: four (one wave per SIMD of a CU, the last blocks
+// three, ocx_pipe_wave_id) unless OCX_BLOCK_WAVES forces another shape or the launch has
+// fewer than four groups.  The few-wave batches measured one-wave blocks (which the plain
+// kernels keep below eight waves per CU) slower: profiles/r04_pipe_bw_ab.jsonl,
+// r04_wave_clock*.jsonl.
+int pipe_block_waves(int64_t G) {
+    if (std::getenv("OCX_BLOCK_WAVES")) return ocx_block_waves(G);
+    return G >= 4 ? 4 : 1;
+}
 bool pipe_spec(int onepass, bool ftl) {
     if (!onepass) return false;
     if (const char* e = std::getenv("OCX_PIPE_SPEC")) return std::atoi(e) != 0;
@@ -656,7 +702,8 @@ hipError_t launch_pipe_k(const ocx_layout* L, const double* zt, const double* yt
     // z_{t-1} .. z_{t+1} must be in the ring, and the late loads (ocx_ring_loop) keep NB-2
     // steps in flight: one slot more than the plain kernel's ring
     constexpr int NB = nb_for(C, P) + 1 < 4 ? 4 : nb_for(C, P) + 1;
-    const dim3 grid = ocx_grid(L->G, ocx_block_waves(L->G)), block(64 * ocx_block_waves(L->G));
+    const int bw = pipe_block_waves(L->G);
+    const dim3 grid = ocx_grid(L->G, bw), block(64 * bw);
     if (!CAND && pipe_fastq(onepass))
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, FTL, false, 1, true>), grid, block, 0,
                            st, zt, yt, L->B, L->T, L->G, eta0, reg, cum, comp, closed_out, onepass,
