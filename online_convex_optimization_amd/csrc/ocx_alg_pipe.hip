@@ -568,6 +568,7 @@ __device__ __forceinline__ void alg_pipe_body(
         return ok;
     };
     if constexpr (CAND) {
+        // ran its own loop and θ_T above
     } else if constexpr (SPEC) {
         if (__ballot(!run_spec()) != 0) {  // wave-uniform: a check failed, start again
 #pragma unroll
