@@ -3,6 +3,11 @@
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one rank per GPU, RCCL)
 
+`python bench.py --gpus N` with N > 1 and no launcher around it starts the N ranks itself
+(launch_ranks: torch.distributed.run as a child process, before anything touches a GPU),
+so both forms measure N GPUs.  Under a launcher --gpus must equal WORLD_SIZE, and an RCCL
+run needs N visible devices: either mismatch exits non-zero instead of sharing a GPU.
+
 A step = one launch of the FTRL kernel (main T-step loop + comparator loss) over
 one resident batch of B sequences per GPU (default B = 32768: a 168 GB resident
 chunk of configs[2]'s 1e5-trial job).  By default the comparator loss of FTL(theta_T)
@@ -204,18 +209,64 @@ def rank_report(dist, rank: int, world: int, ident: dict, elapsed_s: float, kern
             "gathered_blocks_ok": blocks_ok}
 
 
-def main():
-    a = parse()
-    import torch
-    import torch.distributed as dist
-    from online_convex_optimization_amd import engine
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
 
+
+def launch_ranks(n: int, argv, script: str = None) -> int:
+    """`bench.py --gpus N` without a launcher: run `script` (this file) as N ranks of one
+    node through torch.distributed.run, in a child process, and return its exit status.
+    The parent never initialises a GPU (it only parses arguments), so nothing is exec'd
+    from a process holding a HIP context; each rank reads RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* from the environment torchrun gives it, and rank 0 prints the line."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={int(n)}", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", script or os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+    return subprocess.call(cmd, env=env)
+
+
+def rank_env(a, device_count: int):
+    """(world, rank, local rank, GPU index, distributed?) of this process, checked against
+    --gpus: under a launcher --gpus must equal WORLD_SIZE, and an RCCL run needs one device
+    per local rank (a gloo rehearsal may share one).  Raises SystemExit(2) otherwise."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    gpu = local % torch.cuda.device_count() if a.dist_backend == "gloo" else local
+    launched = "WORLD_SIZE" in os.environ
+    if launched and world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        raise SystemExit(2)
+    if a.dist_backend == "nccl" and device_count < world:
+        print(f"bench.py: {world} ranks need {world} GPUs, {device_count} visible",
+              file=sys.stderr)
+        raise SystemExit(2)
+    gpu = local % max(1, device_count) if a.dist_backend == "gloo" else local
     # under torchrun (even with one rank) the process group and the gather are real
     dist_on = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    return world, rank, local, gpu, dist_on
+
+
+def main():
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # no launcher: start the ranks (before any GPU call in this process)
+        import torch
+        n = torch.cuda.device_count()  # counts devices without initialising one
+        if a.dist_backend == "nccl" and n < a.gpus:
+            print(f"bench.py: --gpus {a.gpus} but {n} GPUs visible", file=sys.stderr)
+            raise SystemExit(2)
+        raise SystemExit(launch_ranks(a.gpus, sys.argv[1:]))
+    import torch
+    import torch.distributed as dist
+
+    world, rank, local, gpu, dist_on = rank_env(a, torch.cuda.device_count())
+    from online_convex_optimization_amd import engine
     if dist_on:
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
