@@ -112,6 +112,8 @@ SIGNATURES = {
 TEST_SIGNATURES = {
     "ocx_test_gT_regrets_unclean": (c_int, [c_u64, c_i64, c_i64, c_i64, c_i64, c_double, c_dp,
                                             c_int, c_int, c_i64]),
+    "ocx_test_alg_pipe_chunked": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_i64,
+                                          c_vp, c_vp, c_vp]),
 }
 OCX_VERSION = 400  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1

@@ -69,6 +69,7 @@ struct DevCtx {
     DevBuf zraw, yraw, zt, yt, at, araw, cmp, thr, out, sw;
     DevBuf rstate, lstate, theta, acc;  // long-horizon (T-chunked) g(T) sweep
     DevBuf gmax;                        // ocx_gT_max: the running max's bit pattern
+    DevBuf yt2, gst, fst, bad;          // the trailing pipeline (second label tile, states)
 };
 
 DevCtx g_ctx[kMaxDevices];
@@ -134,6 +135,27 @@ hipError_t launch_max_fold(const double* r, int64_t n, unsigned long long* acc, 
     return hipGetLastError();
 }
 
+// The ocx_dev_* entry points take a stream, not a device: the stream's device is made
+// current for the call (the launchers size their grids from the current device, and
+// ocx_pipeline.hip's library streams and events belong to it) and the caller's restored
+// afterwards.  The null stream is the caller's current device's.
+struct StreamDevice {
+    int prev = -1;
+    explicit StreamDevice(void* stream) {
+        if (!stream) return;
+        int dev = -1, cur = -1;
+        if (hipStreamGetDevice((hipStream_t)stream, &dev) != hipSuccess ||
+            hipGetDevice(&cur) != hipSuccess || dev == cur)
+            return;
+        if (hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~StreamDevice() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    StreamDevice(const StreamDevice&) = delete;
+    StreamDevice& operator=(const StreamDevice&) = delete;
+};
+
 int even_supported_C(int64_t need) {
     static const int Cs[] = {2, 4, 6, 8, 12, 16, 24, 32, 48, 64};
     for (int c : Cs)
@@ -173,7 +195,7 @@ int ocx_release_buffers(int device) {
     OCX_HIP(hipStreamSynchronize(cx->stream));
     for (DevBuf* b : {&cx->zraw, &cx->yraw, &cx->zt, &cx->yt, &cx->at, &cx->araw, &cx->cmp,
                       &cx->thr, &cx->out, &cx->sw, &cx->rstate, &cx->lstate, &cx->theta,
-                      &cx->acc, &cx->gmax})
+                      &cx->acc, &cx->gmax, &cx->yt2, &cx->gst, &cx->fst, &cx->bad})
         OCX_HIP(b->release());
     return OCX_OK;
 }
@@ -290,6 +312,7 @@ static int check_layout(const ocx_layout* L) {
 
 int ocx_dev_pack(const ocx_layout* L, const double* z, const double* y, double* z_tiled,
                  double* y_tiled, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || (L->B * L->T * L->d > 0 && !z)))
         return fail(OCX_E_INVALID, "NULL z buffer");
@@ -300,6 +323,7 @@ int ocx_dev_pack(const ocx_layout* L, const double* z, const double* y, double* 
 
 int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* z_tiled,
                    double* y_tiled, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (run0 < 0) return fail(OCX_E_INVALID, "run0 < 0");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
@@ -310,6 +334,7 @@ int ocx_dev_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double
 int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seeds,
                        const uint64_t* stream_ids, double p, int64_t block_len, double* z_tiled,
                        double* y_tiled, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (family < 1 || family > 4) return fail(OCX_E_INVALID, "family must be 1..4");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
@@ -326,6 +351,7 @@ int ocx_dev_gen_family(const ocx_layout* L, int family, const uint64_t* run_seed
 int ocx_dev_simulate_alg(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                          int alg_flag, double eta0, const double* comparator, double* regret,
                          double* cum_loss, double* comp_loss, double* x_last, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     OCX_HIP(ocx_launch_alg(L, z_tiled, y_tiled, alg_flag != 0 ? 1 : 0, eta0, comparator, regret,
@@ -337,6 +363,7 @@ int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const do
                             int alg_flag, double eta0, const double* comparator, double* regret,
                             double* cum_loss, double* comp_loss, double* x_last, int flags,
                             int32_t* closed_out, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (flags & ~(OCX_ALG_CLIPPED_ROWS | OCX_ALG_CLOSED_COMPARATOR))
@@ -351,6 +378,7 @@ int ocx_dev_simulate_alg_ex(const ocx_layout* L, const double* z_tiled, const do
 int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int norm,
                       double* cum_loss, double* comp_loss, double* cmp_action, int32_t* regime,
                       void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
@@ -363,6 +391,7 @@ int ocx_dev_ftl_exact(const ocx_layout* L, const double* z_tiled, const double* 
 int ocx_dev_ftl_prefix_actions(const ocx_layout* L, const double* z_tiled,
                                const double* y_tiled, int norm, double* actions,
                                int32_t* regime, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
@@ -376,6 +405,7 @@ int ocx_dev_ftl_prefix_actions(const ocx_layout* L, const double* z_tiled,
 int ocx_dev_ftrl_vs_exact(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                           double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                           double* comp_ftl, double* cmp_action, int32_t* regime, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
     if (L->B && (!cum_ftrl || !cum_exact || !comp_exact || !regime))
@@ -389,6 +419,7 @@ int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const d
                              double eta0, double* cum_ftrl, double* cum_exact, double* comp_exact,
                              double* comp_ftl, double* cmp_action, int32_t* regime, int norm,
                              int flags, void* stream) {
+    StreamDevice sd_(stream);
     if (norm < 0 || norm > 2) return fail(OCX_E_INVALID, "norm must be 0 (l2), 1 (l1) or 2 (linf)");
     if (int rc = check_layout(L)) return rc;
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
@@ -409,6 +440,7 @@ int ocx_dev_ftrl_vs_exact_ex(const ocx_layout* L, const double* z_tiled, const d
 int ocx_dev_simulate_smart(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                            const double* thresh, double eta0, double* regret,
                            int64_t* switch_step, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->B && (!thresh || !regret)) return fail(OCX_E_INVALID, "NULL thresh/regret");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
@@ -421,6 +453,7 @@ int ocx_dev_simulate_smart_ex(const ocx_layout* L, const double* z_tiled, const 
                               const double* thresh, double eta0, double* regret,
                               int64_t* switch_step, int flags, unsigned long long* stats,
                               void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->B && (!thresh || !regret)) return fail(OCX_E_INVALID, "NULL thresh/regret");
     if (L->z_elems && (!z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL input buffer");
@@ -441,6 +474,7 @@ int ocx_dev_simulate_smart_ex(const ocx_layout* L, const double* z_tiled, const 
 int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_tiled,
                    const double* y_tiled, const double* a_tiled, double* cum_loss,
                    double* comp_loss, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (int rc = check_layout(La)) return rc;
     if (La->T != L->T + 1 || La->B != L->B || La->P != L->P || La->C != L->C ||
@@ -453,6 +487,7 @@ int ocx_dev_replay(const ocx_layout* L, const ocx_layout* La, const double* z_ti
 }
 
 int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* stream) {
+    StreamDevice sd_(stream);
     if (!gmax || (B > 0 && !regrets)) return fail(OCX_E_INVALID, "NULL buffer");
     OCX_HIP(ocx_launch_max(regrets, B, gmax, (hipStream_t)stream));
     return OCX_OK;
@@ -465,8 +500,8 @@ hipError_t fold_max(const double* r, int64_t n, void* acc, hipStream_t st) {
     return launch_max_fold(r, n, static_cast<unsigned long long*>(acc), st);
 }
 
-// ocx_pipeline.hip's knobs (tuning; the defaults are the measured best): generator waves per
-// SIMD beside the FTRL kernel, and the FTRL step form (candidate-select or plain)
+// ocx_pipeline.hip's knob (tuning; the default is the measured best): generator waves per
+// SIMD beside the FTRL kernel
 int pipe_wps() {
     // 4: four generator waves per SIMD in the 96-VGPR form beside one 128-VGPR FTRL wave;
     // 32 768 x 1e4 x 64 with two streams per side measured 64.3-66.9 ms per batch, vs
@@ -476,10 +511,6 @@ int pipe_wps() {
     const int v = e ? std::atoi(e) : 4;
     return v >= 1 && v <= 8 ? v : 4;
 }
-int pipe_cand_default() {
-    const char* e = std::getenv("OCX_PIPE_CAND");
-    return e ? (std::atoi(e) != 0) : 0;
-}
 }  // namespace
 
 extern "C" {
@@ -487,6 +518,7 @@ extern "C" {
 int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, int64_t nbatch,
                          double* z_tiled, double* y_tiled, double eta0, double* regret,
                          double* gmax, uint32_t flags, int64_t sub_seqs, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (run0 < 0 || nbatch < 0) return fail(OCX_E_INVALID, "negative run0 / nbatch");
     if (flags & ~(OCX_GENSIM_SEQUENTIAL | OCX_GENSIM_TWO_PASS))
@@ -500,13 +532,11 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
     // the reference's streamed pass (the bit-exact modes)
     const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
-    // A stream under HIP graph capture takes the sequential loop: the pipeline forks work to
-    // library streams, and HIP 7's capture crashed ending a capture of that.
-    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) && !ocx_stream_capturing(st) &&
+    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) &&
         (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
                                           regret, onepass, acc ? fold_max : nullptr, acc,
-                                          pipe_wps(), sub_seqs, pipe_cand_default(), st));
+                                          pipe_wps(), sub_seqs, st));
         return OCX_OK;
     }
     for (int64_t k = 0; k < nbatch; ++k) {
@@ -771,6 +801,7 @@ int ocx_replay_batch(const double* z, const double* y, const double* actions, in
 int ocx_dev_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                              int norm, int all_prefixes, double* actions, double* obj, double* gap,
                              double* step_loss, int32_t* info, void* stream) {
+    StreamDevice sd_(stream);
     if (B < 0 || T < 0 || d < 1) return fail(OCX_E_INVALID, "need B >= 0, T >= 0, d >= 1");
     if (d > OCX_EXACT_BALL_MAX_D)
         return fail(OCX_E_UNSUPPORTED, "the general exact-FTL solver takes d <= " +
@@ -787,6 +818,7 @@ int ocx_dev_exact_ball_solve_tiled(const ocx_layout* L, const double* z_tiled,
                                    const double* y_tiled, int norm, int all_prefixes,
                                    double* actions, double* obj, double* gap, double* step_loss,
                                    int32_t* info, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->d < 1) return fail(OCX_E_INVALID, "need d >= 1");
     if (L->d > OCX_EXACT_BALL_MAX_D)
@@ -845,7 +877,8 @@ namespace {
 // fast_algorithms.py:230-243 for one T: the regrets of runs [run0, run0 + R) to the host
 // (`regrets`), or only their max (`gmax`: the regrets never leave the GPU).
 // test_unclean_every (ocx_test_gT_regrets_unclean only, 0 elsewhere): on the streamed path,
-// mark every k-th run as failing the closed form's check, so the fallback pass is exercised.
+// mark every k-th run as failing the closed form's check, so the fallback pass is exercised;
+// on the trailing path, run every k-th batch again whole, as a NaN-flagged batch is.
 // regrets_on_device: `regrets` is device memory of `device` (ocx_gT_regrets_dev): the FTRL
 // kernel writes each batch's regrets straight into it and nothing crosses PCIe.
 int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, double eta0,
@@ -970,14 +1003,77 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         const bool pipe = (!pe || std::atoi(pe) != 0) && ocx_pipeline_supported(&Lp) &&
                           ocx_pipeline_worth(&Lp, pipe_wps());
         int64_t done = 0;
+        // The batches the sub-batch pipeline leaves — capacity-limited (too few generator
+        // rounds to cut: d = 64 at T = 1e5) or d != 64 (configs[4]'s d = 1024) — take the
+        // trailing pipeline (ocx_pipeline.hip): batch k+1 generated chunk by chunk behind the
+        // chunked FTRL pass over batch k, in the same z buffer (OCX_TRAILING=0: the sequential
+        // loop below).  Its second label tile comes out of the budget.
+        const char* te = std::getenv("OCX_TRAILING");
+        bool trail = !pipe && onepass && (!te || std::atoi(te) != 0) &&
+                     ocx_trailing_supported(&Lp) && R / chunk >= 2;
+        if (trail) {
+            const int64_t per_trail = per_seq + 8 * T + 64 * 8 * (2 * (int64_t)Lp.C + 7);
+            int64_t c2 = std::max<int64_t>(64, std::min<int64_t>(budget / per_trail, R));
+            const int64_t nb2 = (R + c2 - 1) / c2;
+            c2 = (R + nb2 - 1) / nb2;
+            if (c2 < chunk) {
+                chunk = c2;
+                if (int rc = ocx_layout_init(chunk, T, d, lanes_per_seq, &Lp)) return rc;
+                OCX_HIP(cx->out.ensure((size_t)chunk * 8));
+            }
+            trail = ocx_trailing_supported(&Lp) && R / chunk >= 2;
+        }
+        if (trail) {
+            const int64_t nfull = R / chunk;
+            OCX_HIP(cx->zt.ensure((size_t)Lp.z_elems * 8));
+            OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
+            OCX_HIP(cx->yt2.ensure((size_t)Lp.y_elems * 8));
+            OCX_HIP(cx->gst.ensure((size_t)2 * Lp.G * Lp.S * 6 * 8));
+            OCX_HIP(cx->fst.ensure((size_t)ocx_pipe_state_doubles(&Lp) * 8));
+            OCX_HIP(cx->bad.ensure((size_t)nfull * sizeof(int)));
+            double* rdst = regrets_on_device ? regrets : nullptr;
+            if (!rdst) {
+                OCX_HIP(cx->out.ensure((size_t)(nfull * chunk) * 8));
+                rdst = cx->out.as<double>();
+            }
+            int nch = 8;  // FTRL chunks per horizon (OCX_TRAIL_CHUNKS, tuning)
+            if (const char* e = std::getenv("OCX_TRAIL_CHUNKS")) nch = std::max(2, std::atoi(e));
+            OCX_HIP(ocx_run_gen_sim_trailing(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
+                                             cx->yt.as<double>(), cx->yt2.as<double>(),
+                                             cx->gst.as<uint64_t>(), cx->fst.as<double>(),
+                                             cx->bad.as<int>(), eta0, rdst,
+                                             dmax ? fold_max : nullptr, dmax, nch, st));
+            // a batch with a sequence the closed-form comparator could not certify (its regret
+            // NaN, never the max) runs again whole: the kernel streams its second pass
+            std::vector<int> hb((size_t)nfull, 0);
+            OCX_HIP(hipMemcpyAsync(hb.data(), cx->bad.p, (size_t)nfull * sizeof(int),
+                                   hipMemcpyDeviceToHost, st));
+            OCX_HIP(hipStreamSynchronize(st));
+            if (test_unclean_every > 0)  // test hook: these batches run again as if marked
+                for (int64_t k = 0; k < nfull; k += test_unclean_every) hb[(size_t)k] = 1;
+            for (int64_t k = 0; k < nfull; ++k) {
+                if (!hb[(size_t)k]) continue;
+                OCX_HIP(ocx_launch_gen_gT(&Lp, base_seed, run0 + k * chunk, cx->zt.as<double>(),
+                                          cx->yt.as<double>(), st));
+                OCX_HIP(ocx_launch_alg(&Lp, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0,
+                                       nullptr, rdst + k * chunk, nullptr, nullptr, nullptr, st,
+                                       nullptr, nullptr, onepass));
+                if (dmax) OCX_HIP(launch_max_fold(rdst + k * chunk, chunk, dmax, st));
+            }
+            if (!dmax && !regrets_on_device) {
+                OCX_HIP(hipMemcpyAsync(regrets, rdst, (size_t)(nfull * chunk) * 8,
+                                       hipMemcpyDeviceToHost, st));
+                OCX_HIP(hipStreamSynchronize(st));
+            }
+            done = nfull * chunk;
+        }
         if (pipe && dmax) {
             const int64_t nfull = R / chunk;
             OCX_HIP(cx->zt.ensure((size_t)Lp.z_elems * 8));
             OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
             OCX_HIP(ocx_run_gen_sim_pipelined(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
                                               cx->yt.as<double>(), eta0, cx->out.as<double>(),
-                                              onepass, fold_max, dmax, pipe_wps(), 0,
-                                              pipe_cand_default(), st));
+                                              onepass, fold_max, dmax, pipe_wps(), 0, st));
             done = nfull * chunk;
         }
         for (int64_t r0 = done; r0 < R; r0 += chunk) {
@@ -990,8 +1086,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             if (pipe && ocx_pipeline_supported(&L) && ocx_pipeline_worth(&L, pipe_wps())) {
                 OCX_HIP(ocx_run_gen_sim_pipelined(&L, base_seed, run0 + r0, 1, cx->zt.as<double>(),
                                                   cx->yt.as<double>(), eta0, rdst, onepass,
-                                                  nullptr, nullptr, pipe_wps(), 0,
-                                                  pipe_cand_default(), st));
+                                                  nullptr, nullptr, pipe_wps(), 0, st));
             } else {
                 OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
                                           cx->yt.as<double>(), st));
@@ -1103,6 +1198,28 @@ int ocx_gT_regrets_dev(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, i
     if (!regrets_dev && R > 0) return fail(OCX_E_INVALID, "NULL regrets");
     return gT_run(base_seed, T, run0, R, d, eta0, regrets_dev, nullptr, lanes_per_seq, device, 0,
                   true);
+}
+
+int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
+                              double eta0, int64_t chunk_steps, double* regret, int* bad,
+                              void* stream) {
+    StreamDevice sd_(stream);
+    if (int rc = check_layout(L)) return rc;
+    if (!ocx_pipe_supported(L)) return fail(OCX_E_UNSUPPORTED, "not a pipelined butterfly layout");
+    if (chunk_steps <= 0 || chunk_steps % 64) return fail(OCX_E_INVALID, "chunk_steps: a multiple of 64");
+    if (L->B > 0 && (!regret || !bad || !z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
+    const hipStream_t st = (hipStream_t)stream;
+    double* state = nullptr;
+    OCX_HIP(hipMalloc(&state, (size_t)std::max<int64_t>(ocx_pipe_state_doubles(L), 1) * 8));
+    hipError_t e = hipSuccess;
+    for (int64_t t0 = 0; t0 < L->T && e == hipSuccess; t0 += chunk_steps)
+        e = ocx_launch_alg_pipe_chunk(L, z_tiled, y_tiled, eta0, regret, 1, t0,
+                                      std::min(chunk_steps, L->T - t0), state, bad, st);
+    const hipError_t es = hipStreamSynchronize(st);
+    (void)hipFree(state);
+    OCX_HIP(e);
+    OCX_HIP(es);
+    return OCX_OK;
 }
 
 int ocx_test_gT_regrets_unclean(uint64_t base_seed, int64_t T, int64_t run0, int64_t R,
@@ -1249,6 +1366,7 @@ int ocx_twin32_batch(const float* z, const float* y, int64_t B, int64_t T, int64
 int ocx_dev_twin32(const ocx_layout* L, const double* z_tiled, const double* y_tiled, int algo,
                    double eta0, const double* thresh, float* result, double* cum_loss,
                    float* comp_loss, int64_t* switch_step, void* stream) {
+    StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
     if (L->P != 1) return fail(OCX_E_INVALID, "the float32 twin needs a one-lane layout (lanes_per_seq = -1)");
     if (L->d > 32) return fail(OCX_E_UNSUPPORTED, "the float32 twin supports d <= 32");

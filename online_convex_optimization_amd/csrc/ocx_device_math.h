@@ -61,15 +61,20 @@ constexpr int nb_for(int C, int P = 1, bool deep = true) {
 // keeps the loop's bound and clamp tests on the scalar unit: the ISA has no 64-bit signed
 // scalar compare, so an int64_t counter costs two VALU compares per step whose results the
 // scalar unit then waits for.
+// T_load (>= T_arg; default T_arg): the rows that exist for the loads — a chunk of a longer
+// horizon (ocx_alg_pipe_kernel's chunked runs) looks ahead into the next chunk's rows, and
+// only the horizon's last row clamps.
 template <int NB, bool LATE = false, class IT = int64_t, class Load, class Step>
-__device__ __forceinline__ void ocx_ring_loop(int64_t T_arg, Load&& load, Step&& step) {
+__device__ __forceinline__ void ocx_ring_loop(int64_t T_arg, Load&& load, Step&& step,
+                                              int64_t T_load = -1) {
     static_assert(NB >= (LATE ? 3 : 2), "a ring with at least one step in flight");
     constexpr int BL = NB * OCX_RING_UNROLL;  // steps per loop iteration
     if (T_arg <= 0) return;
     const IT T = (IT)T_arg;
+    const IT TL = T_load < T_arg ? T : (IT)T_load;
 #pragma unroll
     for (int u = 0; u < NB - 1; ++u) {
-        load(u, (int64_t)(u < T ? (IT)u : T - 1));
+        load(u, (int64_t)(u < TL ? (IT)u : TL - 1));
         // keep the prologue's loads in slot order: the loop header merges this order with
         // the back edge's, and a slot the scheduler loaded last here would be waited for
         // as if it were the newest load on every pass (a drain once per ring cycle)
@@ -79,9 +84,9 @@ __device__ __forceinline__ void ocx_ring_loop(int64_t T_arg, Load&& load, Step&&
 #pragma unroll
         for (int u = 0; u < BL; ++u) {
             const IT tp = t0 + u + NB - 1;
-            if (!LATE) load((u + NB - 1) % NB, (int64_t)(tp < T ? tp : T - 1));  // unconditional: above
+            if (!LATE) load((u + NB - 1) % NB, (int64_t)(tp < TL ? tp : TL - 1));  // unconditional: above
             if (t0 + u < T) step(u % NB, (int64_t)(t0 + u));  // the last block may be short
-            if (LATE) load((u + NB - 1) % NB, (int64_t)(tp < T ? tp : T - 1));
+            if (LATE) load((u + NB - 1) % NB, (int64_t)(tp < TL ? tp : TL - 1));
         }
     }
 }

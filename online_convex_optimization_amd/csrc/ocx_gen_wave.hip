@@ -894,10 +894,11 @@ constexpr int kRows64 = 8;
 
 }  // namespace
 
-// MODE 0 (generate): rows [0, T) of the tiled layout (z_t clipped, fast_algorithms.py:
-//   234-237) and then the labels (:239).  Fresh streams _rng(base_seed, T_seed, run0+b),
-//   or, in chunk mode (st_in != nullptr), rows resume from st_in[b] (saved to st_out[b])
-//   and labels from lab_in[b] (saved to lab_out[b]).
+// MODE 0 (generate): rows [t_off, t_off + nrows) of the tiled layout (z_t clipped,
+//   fast_algorithms.py:234-237; a whole launch: [0, T)) and then, if `labels`, the T labels
+//   (:239).  Fresh streams _rng(base_seed, T_seed, run0+b), or, in chunk mode (st_in !=
+//   nullptr), rows resume from st_in[b]; the stream after the rows is saved to st_out[b]
+//   (nullable), and the labels resume from lab_in[b] (saved to lab_out[b]) when given.
 // MODE 1 (seek): st_out[b] = the fresh stream, lab_out[b] = the stream after its
 //   T_seed·d normals, i.e. where choice(T) starts.
 // DF = 64: the d = 64, P·C = 64 rows of every configs[] workload, with the row shape
@@ -920,7 +921,7 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
     int d_arg, int P, int C, int64_t G, double* __restrict__ zt, double* __restrict__ ytl,
     const uint64_t* __restrict__ st_in, uint64_t* __restrict__ st_out,
     const uint64_t* __restrict__ lab_in, uint64_t* __restrict__ lab_out, int rb,
-    int64_t nwaves, int64_t b_off) {
+    int64_t nwaves, int64_t b_off, int64_t t_off, int64_t nrows, int labels) {
     constexpr int kBlock = gen_block(DF, LR, OV);
     constexpr int kNW = kBlock / 64;
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
@@ -1022,8 +1023,9 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             return zt + (((int64_t)(rr >> 1) * G + g) * T + t) * 128 + (s * P + c) * 2 + (rr & 1);
         };
         if (MODE == 0 && (b >= B || d == 0)) {  // padding sequence / empty rows: zeros
-            for (int64_t t = 0; t < T; ++t)
+            for (int64_t t = t_off; t < t_off + nrows; ++t)
                 for (int j = lane; j < Dp; j += 64) *zaddr(t, j) = 0.0;
+            if (b >= B && !labels) continue;
             if (b >= B) {
                 if (stage_y) {
                     // the block's label rounds (and barriers) with zeros for this sequence
@@ -1057,10 +1059,10 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             // first); the last batch may be shorter.  The batch's row scales reach the store
             // lanes through LDS (`scl`, one broadcast read per row) instead of readlanes.
             constexpr int RR = kRows64;
-            const uint32_t total = (uint32_t)(T * 64);
+            const uint32_t total = (uint32_t)(nrows * 64);
             uint32_t produced = 0;
             unsigned head = 0;  // normals in the ring
-            int64_t t = 0;
+            int64_t t = t_off;
             double* scl = ring + RR * 64 + 64;  // the batch's row scales
             // deferred wedges (the default form): the pending list and the removed-slot flags
             // follow the scales in the wave's slot (ring_doubles)
@@ -1134,10 +1136,10 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             constexpr int kFlat = 2047;  // every ring index is < 1088: masking is a no-op
             constexpr int kSW = OCX_GEN_SWZ1K ? 1 : 0;
             constexpr bool kF1k = OCX_GEN_1K_FLAT;
-            const uint32_t total = (uint32_t)(T * 1024);
+            const uint32_t total = (uint32_t)(nrows * 1024);
             uint32_t produced = 0;
             unsigned head = 0;
-            int64_t t = 0;
+            int64_t t = t_off;
             const int64_t kst = G * T * 128;
             const double* rp = ring + st1k.j0;
             const int64_t pstep = st1k.kstep * kst;
@@ -1213,12 +1215,12 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
                 }
             }
         } else {
-        const int64_t rows = (MODE == 0) ? T : T_seed;
+        const int64_t rows = (MODE == 0) ? nrows : T_seed;
         uint32_t remaining = (uint32_t)(rows * d);  // normals still to draw (< 2^32, host-checked)
         unsigned head = 0, tailp = 0;  // ring counters (mod 2^32; masked on use)
         unsigned partial = 0;          // normals of the row being filled
         int ready = 0;                 // whole rows waiting in the ring
-        int64_t t = 0;
+        int64_t t = t_off;
         while (remaining > 0) {
             int need = remaining < 64 ? (int)remaining : 64;
             const int n = zig_round<MODE == 0>(w, need, tb, ring, rmask, head, lane);
@@ -1304,8 +1306,8 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             if (lane == 0) save_state6(lab_out + 6 * b, w.base, w.inc, 0, 0);
             continue;
         }
-        if (st_in != nullptr && st_out != nullptr && lane == 0)
-            save_state6(st_out + 6 * b, w.base, w.inc, 0, 0);
+        if (st_out != nullptr && lane == 0) save_state6(st_out + 6 * b, w.base, w.inc, 0, 0);
+        if (!labels) continue;
 
         // ---- labels: choice([-1., 1.], T) = top bit of each buffered uint32, low half first
         uint32_t buf32 = 0;
@@ -1364,7 +1366,8 @@ template <int MODE, int DF, bool LR = false, bool RAW = false>
 hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B,
                           int64_t nseq, int64_t T, int64_t d, int P, int C, int64_t G, double* zt,
                           double* ytl, const uint64_t* st_in, uint64_t* st_out,
-                          const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st) {
+                          const uint64_t* lab_in, uint64_t* lab_out, hipStream_t st,
+                          int64_t t_off = 0, int64_t nrows = -1, int labels = 1) {
     constexpr int kBlock = gen_block(DF, LR);
     const int rb = (MODE == 0) ? ring_doubles(d, DF, LR) : 0;
     const size_t lds =
@@ -1414,7 +1417,8 @@ hipError_t launch_wave_df(uint64_t base_seed, int64_t T_seed, int64_t run0, int6
     const int64_t nwaves = (int64_t)blocks * (kBlock / 64);
     hipLaunchKernelGGL((ocx_gen_wave_kernel<MODE, DF, LR, RAW>), dim3(blocks), dim3(kBlock), lds, st,
                        base_seed, T_seed, run0, B, nseq, T, (int)d, P, C, G, zt, ytl, st_in,
-                       st_out, lab_in, lab_out, rb, nwaves, (int64_t)0);
+                       st_out, lab_in, lab_out, rb, nwaves, (int64_t)0, t_off, nrows < 0 ? T : nrows,
+                       labels);
     return hipGetLastError();
 }
 
@@ -1460,7 +1464,7 @@ OvGeom ov_geometry(int dev, int wps) {
 
 hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                    int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
-                                   hipStream_t st, int form96) {
+                                   hipStream_t st) {
     if (nseq <= 0 || L->T == 0) return hipSuccess;
     if (L->d != 64 || L->P * L->C != 64 || b_off % 4 || nseq % 4) return hipErrorInvalidValue;
     if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
@@ -1470,8 +1474,8 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
     e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (e != hipSuccess) return e;
     // up to three waves per SIMD the 128-VGPR form (one FTRL wave of <= 128 VGPRs fits
-    // beside it); four: the 96-VGPR form (a few spills)
-    const bool w4 = wps >= 4 || form96;
+    // beside it); four or more: the 96-VGPR form (a few spills)
+    const bool w4 = wps >= 4;
     const OvGeom gm = w4 ? ov_geometry<5>(dev, wps) : ov_geometry<4>(dev, wps);
     const int64_t resident = (int64_t)cus * 4 * std::max(1, std::min(gm.per_cu, wps));
     const int64_t per_wave = (nseq + resident - 1) / resident;
@@ -1482,13 +1486,13 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
                            gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
                            (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
                            (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                           ring_doubles(64, 64), nwaves, b_off);
+                           ring_doubles(64, 64), nwaves, b_off, (int64_t)0, L->T, 1);
     else
         hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, 4>), dim3(blocks), dim3(256),
                            gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
                            (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
                            (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                           ring_doubles(64, 64), nwaves, b_off);
+                           ring_doubles(64, 64), nwaves, b_off, (int64_t)0, L->T, 1);
     return hipGetLastError();
 }
 
@@ -1508,7 +1512,7 @@ hipError_t ocx_launch_gen_gT_range_lr(const ocx_layout* L, uint64_t base_seed, i
                        st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d, (int)L->P,
                        (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                        (const uint64_t*)nullptr, (uint64_t*)nullptr, rb, (int64_t)blocks * (kBlock / 64),
-                       b_off);
+                       b_off, (int64_t)0, L->T, 1);
     return hipGetLastError();
 }
 
@@ -1518,7 +1522,8 @@ template <int MODE>
 hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t B, int64_t nseq,
                        int64_t T, int64_t d, int P, int C, int64_t G, double* zt, double* ytl,
                        const uint64_t* st_in, uint64_t* st_out, const uint64_t* lab_in,
-                       uint64_t* lab_out, hipStream_t st) {
+                       uint64_t* lab_out, hipStream_t st, int64_t t_off = 0, int64_t nrows = -1,
+                       int labels = 1) {
     // the kernel counts a sequence's normals in 32 bits
     if ((MODE == 0 ? T : T_seed) * d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
     if (d == 64 && (MODE == 1 || (int64_t)P * C == 64)) {
@@ -1548,15 +1553,17 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
         bool lr = l6 < l4 || (wps6 > wps4 && (double)l6 <= 1.06 * (double)l4);
         if (MODE == 0 && lr)
             return launch_wave_df<MODE, 64, true>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G,
-                                                  zt, ytl, st_in, st_out, lab_in, lab_out, st);
+                                                  zt, ytl, st_in, st_out, lab_in, lab_out, st,
+                                                  t_off, nrows, labels);
         return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
-                                        st_in, st_out, lab_in, lab_out, st);
+                                        st_in, st_out, lab_in, lab_out, st, t_off, nrows, labels);
     }
     if (MODE == 0 && d == 1024 && (int64_t)P * C == 1024 && P <= 64)
         return launch_wave_df<MODE, 1024>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt,
-                                          ytl, st_in, st_out, lab_in, lab_out, st);
+                                          ytl, st_in, st_out, lab_in, lab_out, st, t_off, nrows,
+                                          labels);
     return launch_wave_df<MODE, 0>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
-                                   st_in, st_out, lab_in, lab_out, st);
+                                   st_in, st_out, lab_in, lab_out, st, t_off, nrows, labels);
 }
 
 }  // namespace
@@ -1566,11 +1573,9 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
     const int64_t nseq = L->G * L->S;
     if (nseq == 0 || L->T == 0) return hipSuccess;
     // d = 64 batches of four or more generator rounds: one round per launch over two streams
-    // (ocx_run_gen_rounds), bit-identical; OCX_GEN_ROUNDS=0 keeps the single launch (tuning),
-    // and so does a stream under graph capture (the rounds fork to a library stream)
+    // (ocx_run_gen_rounds), bit-identical; OCX_GEN_ROUNDS=0 keeps the single launch (tuning)
     const char* gr = std::getenv("OCX_GEN_ROUNDS");
-    if ((!gr || std::atoi(gr) != 0) && ocx_pipeline_supported(L) && ocx_pipeline_worth(L, 4) &&
-        !ocx_stream_capturing(st))
+    if ((!gr || std::atoi(gr) != 0) && ocx_pipeline_supported(L) && ocx_pipeline_worth(L, 4))
         return ocx_run_gen_rounds(L, base_seed, run0, zt, ytl, st);
     return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt,
                           ytl, nullptr, nullptr, nullptr, nullptr, st);
@@ -1600,4 +1605,20 @@ hipError_t ocx_launch_gen_gT_chunk(const ocx_layout* L, int64_t T_seed, const ui
     if (nseq == 0 || L->T == 0) return hipSuccess;
     return launch_wave<0>(0, T_seed, 0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt, ytl, st_in,
                           st_out, lab_in, lab_out, st);
+}
+
+// Rows [t_off, t_off + nrows) of every sequence of L's full-horizon tile (the trailing
+// pipeline, ocx_pipeline.hip): fresh streams _rng(base_seed, L->T, run0 + b) when st_in is
+// null, else resumed from st_in[b]; the stream after the rows is saved to st_out[b]
+// (nullable; a buffer other than st_in).  labels: the last row range of a horizon also draws the T
+// labels that follow its normals (fast_algorithms.py:239), as a whole-horizon launch does.
+hipError_t ocx_launch_gen_gT_rows(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                  int64_t t_off, int64_t nrows, const uint64_t* st_in,
+                                  uint64_t* st_out, int labels, double* zt, double* ytl,
+                                  hipStream_t st) {
+    const int64_t nseq = L->G * L->S;
+    if (nseq == 0 || L->T == 0 || nrows <= 0) return hipSuccess;
+    if (t_off < 0 || t_off + nrows > L->T) return hipErrorInvalidValue;
+    return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt, ytl,
+                          st_in, st_out, nullptr, nullptr, st, t_off, nrows, labels);
 }

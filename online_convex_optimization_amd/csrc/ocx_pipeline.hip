@@ -35,7 +35,10 @@ struct PipeCtx {
     bool init = false;
     hipStream_t sim = nullptr;
     hipStream_t gen2 = nullptr, sim2 = nullptr;  // the second generator / FTRL streams
-    hipEvent_t join_gen2 = nullptr, join_sim2 = nullptr, fork = nullptr;
+    // fork: the caller's work so far (every library stream waits on it); join_*: each library
+    // stream's last work, waited on by the caller's stream.  One event per role, so no event
+    // is re-recorded within a call (a captured call then has one producer per event)
+    hipEvent_t fork = nullptr, join_gen2 = nullptr, join_sim = nullptr, join_sim2 = nullptr;
     std::vector<hipEvent_t> ev_gen, ev_sim;
     std::vector<char> sim_recorded;
 };
@@ -62,6 +65,7 @@ hipError_t pipe_init(PipeCtx& c) {  // under c.mu
     if ((e = hipStreamCreateWithFlags(&c.gen2, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipStreamCreateWithFlags(&c.sim2, hipStreamNonBlocking)) != hipSuccess) return e;
     if ((e = hipEventCreateWithFlags(&c.join_gen2, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&c.join_sim, hipEventDisableTiming)) != hipSuccess) return e;
     if ((e = hipEventCreateWithFlags(&c.join_sim2, hipEventDisableTiming)) != hipSuccess) return e;
     if ((e = hipEventCreateWithFlags(&c.fork, hipEventDisableTiming)) != hipSuccess) return e;
     c.init = true;
@@ -85,11 +89,6 @@ int64_t lcm64(int64_t a, int64_t b) {
     } while (0)
 
 }  // namespace
-
-bool ocx_stream_capturing(hipStream_t st) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-}
 
 bool ocx_pipeline_supported(const ocx_layout* L) {
     return L->d == 64 && L->P * L->C == 64 && ocx_pipe_lean_supported(L) && L->T > 0 &&
@@ -142,7 +141,7 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
         OCX_PIPE_TRY(lr6 ? ocx_launch_gen_gT_range_lr(L, base_seed, run0, b0, std::min(sub, Bp - b0),
                                                       zt, yt, (j & 1) ? c.gen2 : st)
                          : ocx_launch_gen_gT_range(L, base_seed, run0, b0, std::min(sub, Bp - b0),
-                                                   wps, zt, yt, (j & 1) ? c.gen2 : st, 1));
+                                                   wps, zt, yt, (j & 1) ? c.gen2 : st));
     OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
     OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
     return hipSuccess;
@@ -157,8 +156,7 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
                                      int64_t nbatch, double* zt, double* yt, double eta0,
                                      double* regret, int onepass,
                                      hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
-                                     void* fold_arg, int wps, int64_t sub_seqs, int cand,
-                                     hipStream_t st) {
+                                     void* fold_arg, int wps, int64_t sub_seqs, hipStream_t st) {
     if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
     int dev = 0, cus = 256;
     OCX_PIPE_TRY(hipGetDevice(&dev));
@@ -180,9 +178,11 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     const char* ss_env = std::getenv("OCX_PIPE_SIM_STREAMS");
     const int ngs = (gs_env && std::atoi(gs_env) == 1) ? 1 : 2;
     const int nss = (ss_env && std::atoi(ss_env) == 1) ? 1 : 2;
-    // the extra streams start after the work already queued on the caller's stream
+    // the library streams start after the work already queued on the caller's stream: each
+    // waits on the fork (under graph capture that wait is what makes it join the capture)
     OCX_PIPE_TRY(hipEventRecord(c.fork, st));
     OCX_PIPE_TRY(hipStreamWaitEvent(c.gen2, c.fork, 0));
+    OCX_PIPE_TRY(hipStreamWaitEvent(c.sim, c.fork, 0));
     OCX_PIPE_TRY(hipStreamWaitEvent(c.sim2, c.fork, 0));
     const int64_t S = L->S;
     const int64_t Bp = L->G * S;  // sequences of the layout, padding included
@@ -200,16 +200,13 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     const int64_t nsub = (Bp + sub - 1) / sub;
     OCX_PIPE_TRY(ensure_events(c, (size_t)nsub));
     std::fill(c.sim_recorded.begin(), c.sim_recorded.end(), 0);
-    // tuning only (wrong outputs): time one side of the pipeline alone
+#ifdef OCX_PIPE_TUNE_SKIP
+    // tuning builds only (wrong outputs): time one side of the pipeline alone
     const char* sk = std::getenv("OCX_PIPE_SKIP");
     const bool skip_gen = sk && sk[0] == 'g', skip_sim = sk && sk[0] == 's';
-    // the FTRL side's register budget (tuning, OCX_PIPE_LEAN): 128 VGPRs beside three
-    // generator waves of the 128-VGPR form or four of the 96-VGPR one; 168 beside three of
-    // the 96-VGPR form
-    const char* lb = std::getenv("OCX_PIPE_LEAN");
-    const int sim_budget = lb ? std::atoi(lb) : 128;
-    // the generator's register form: 96 VGPRs when the FTRL side takes 168 (or at wps 4)
-    const int gen96 = sim_budget >= 168 ? 1 : 0;
+#else
+    constexpr bool skip_gen = false, skip_sim = false;
+#endif
     int64_t j = 0;  // sub-batch launches so far (stream alternation)
     for (int64_t k = 0; k < nbatch; ++k) {
         const int64_t r0 = run0 + k * L->B;
@@ -220,12 +217,11 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
             // this region's previous reader (sub-batch i of batch k-1) must be done
             if (c.sim_recorded[(size_t)i]) OCX_PIPE_TRY(hipStreamWaitEvent(gs, c.ev_sim[(size_t)i], 0));
             if (!skip_gen)
-                OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, gs, gen96));
+                OCX_PIPE_TRY(ocx_launch_gen_gT_range(L, base_seed, r0, b0, nb, wps, zt, yt, gs));
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], gs));
             OCX_PIPE_TRY(hipStreamWaitEvent(ss, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
-                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
-                                                      cand, ss, sim_budget));
+                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S, ss));
             const int64_t nreal = std::min(nb, L->B - b0);
             if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, ss));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], ss));
@@ -234,13 +230,91 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     }
     // the caller's stream sees every generator launch, FTRL pass and fold done (each stream
     // runs in order: its last event covers it)
-    if (nsub > 0 && nbatch > 0) {
-        OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
-        OCX_PIPE_TRY(hipEventRecord(c.join_sim2, c.sim2));
-        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
-        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim2, 0));
-        OCX_PIPE_TRY(hipEventRecord(c.fork, c.sim));
-        OCX_PIPE_TRY(hipStreamWaitEvent(st, c.fork, 0));
+    OCX_PIPE_TRY(hipEventRecord(c.join_gen2, c.gen2));
+    OCX_PIPE_TRY(hipEventRecord(c.join_sim, c.sim));
+    OCX_PIPE_TRY(hipEventRecord(c.join_sim2, c.sim2));
+    OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_gen2, 0));
+    OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim, 0));
+    OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim2, 0));
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The trailing pipeline: generation of batch k+1 overlapped with the FTRL pass over batch k
+// INSIDE ONE z buffer, for the batches the HBM budget caps (d = 64 at T = 1e5: ≈4 900 streams;
+// d = 1024 at T = 1e4: ≈2 700), where a double buffer would halve the batch and the sub-batch
+// pipeline above has too few generator rounds to cut.  The horizon is cut into n chunks of
+// whole 64-step blocks.  FTRL over batch k runs chunk by chunk (ocx_launch_alg_pipe_chunk:
+// the step's state carried through HBM, bit-identical to one launch), and the generator of
+// batch k+1 writes chunk c's rows (ocx_launch_gen_gT_rows: the stream resumed from the state
+// chunk c−1 left) as soon as FTRL k has read them — an event per chunk orders that — so the
+// generator trails the reader through the same rows.  NumPy draws a sequence's labels after
+// all of its T·d normals (fast_algorithms.py:234-239), so the last chunk's launch draws them,
+// into the other of two label tiles (y is 1/d of z); FTRL k+1 starts when that is done.
+// Per batch the FTRL pass then hides behind generation except for its first chunk.
+//
+// z, y[2]: the layout's tiles; gst: 2·(G·S)·6 words of generator states (ping-pong);
+// fst: ocx_pipe_state_doubles(L); bad[nbatch]: set for a batch with a sequence the closed-form
+// comparator could not certify (its regret is NaN: the caller reruns that batch whole);
+// regret: nbatch·B doubles, batch k's at regret + k·B; fold(regret_k, B, fold_arg, stream)
+// after each batch (nullable).
+bool ocx_trailing_supported(const ocx_layout* L) {
+    return ocx_pipe_supported(L) && L->T >= 128 && L->T * L->d < ((int64_t)1 << 32);
+}
+
+hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                    int64_t nbatch, double* zt, double* yt0, double* yt1,
+                                    uint64_t* gst, double* fst, int* bad, double eta0,
+                                    double* regret,
+                                    hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
+                                    void* fold_arg, int nchunks, hipStream_t st) {
+    if (!ocx_trailing_supported(L) || nbatch <= 0 || !regret || !gst || !fst || !bad)
+        return hipErrorInvalidValue;
+    int dev = 0;
+    OCX_PIPE_TRY(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    PipeCtx& c = g_pipe[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    OCX_PIPE_TRY(pipe_init(c));
+    // chunks of whole 64-step blocks (the FTRL state's refresh points), at least two
+    const int64_t blocks = (L->T + 63) / 64;
+    const int64_t n = std::max<int64_t>(2, std::min<int64_t>(nchunks, blocks));
+    const int64_t tc = (blocks + n - 1) / n * 64;
+    const int64_t nch = (L->T + tc - 1) / tc;
+    OCX_PIPE_TRY(ensure_events(c, (size_t)nch));
+    const int64_t words = L->G * L->S * 6;
+    double* yts[2] = {yt0, yt1};
+    hipStream_t F = c.sim;
+    OCX_PIPE_TRY(hipMemsetAsync(bad, 0, (size_t)nbatch * sizeof(int), st));
+    // batch 0 in one launch (the plain one: ocx_launch_gen_gT's rounds would take this lock);
+    // the FTRL stream starts after it and after the caller's work
+    OCX_PIPE_TRY(ocx_launch_gen_gT_rows(L, base_seed, run0, 0, L->T, nullptr, nullptr, 1, zt, yt0, st));
+    for (int64_t k = 0; k < nbatch; ++k) {
+        // FTRL k: batch k is generated (its last launch was queued on st just before)
+        OCX_PIPE_TRY(hipEventRecord(c.fork, st));
+        OCX_PIPE_TRY(hipStreamWaitEvent(F, c.fork, 0));
+        double* yk = yts[k & 1];
+        for (int64_t ci = 0; ci < nch; ++ci) {
+            const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
+            OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(L, zt, yk, eta0, regret + k * L->B, 1, t0, tn,
+                                                   fst, bad + k, F));
+            OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)ci], F));
+        }
+        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, L->B, fold_arg, F));
+        if (k + 1 == nbatch) break;
+        // batch k+1, chunk by chunk behind FTRL k; its labels with the last chunk
+        const int64_t rk = run0 + (k + 1) * L->B;
+        for (int64_t ci = 0; ci < nch; ++ci) {
+            const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
+            const bool lastc = ci + 1 == nch;
+            OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)ci], 0));
+            OCX_PIPE_TRY(ocx_launch_gen_gT_rows(L, base_seed, rk, t0, tn,
+                                                ci == 0 ? nullptr : gst + ((ci - 1) & 1) * words,
+                                                lastc ? nullptr : gst + (ci & 1) * words,
+                                                lastc ? 1 : 0, zt, yts[(k + 1) & 1], st));
+        }
     }
+    OCX_PIPE_TRY(hipEventRecord(c.join_sim, F));
+    OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim, 0));
     return hipSuccess;
 }

@@ -465,9 +465,16 @@ class DeviceBatch:
     def _lp(self):
         return ctypes.byref(self.L)
 
+    def _call(self, name, *args):
+        """_lib.call with this batch's device current: the null stream of a torch device is
+        the current device's, and the library sizes its launches and forks its streams
+        from the current device (a DeviceBatch on device 1 works without set_device)."""
+        with self.torch.cuda.device(self.device):
+            return _lib.call(name, *args)
+
     def generate_gT(self, base_seed: int = 0, run0: int = 0):
         """Fill z/y with _rng(base_seed, T, run0 + b) sequences (on device)."""
-        _lib.call("ocx_dev_gen_gT", self._lp(), int(base_seed), int(run0), self.z.data_ptr(),
+        self._call("ocx_dev_gen_gT", self._lp(), int(base_seed), int(run0), self.z.data_ptr(),
                   self.y.data_ptr(), self._sp)
         self.rows_clipped = True
         return self
@@ -490,7 +497,7 @@ class DeviceBatch:
             if rs.numel() != self.L.B or si.numel() != self.L.B:
                 raise ValueError("need one run seed and one stream id per sequence")
         self.rows_clipped = False
-        _lib.call("ocx_dev_gen_family", self._lp(), fam,
+        self._call("ocx_dev_gen_family", self._lp(), fam,
                   rs.data_ptr() if rs is not None else None,
                   si.data_ptr() if si is not None else None, float(p), int(block_len),
                   self.z.data_ptr(), self.y.data_ptr(), self._sp)
@@ -510,7 +517,7 @@ class DeviceBatch:
         if tuple(zt.shape) != (self.L.B, self.L.T, self.L.d) or tuple(yt.shape) != (self.L.B, self.L.T):
             raise ValueError("z/y shape does not match the batch")
         self.rows_clipped = False
-        _lib.call("ocx_dev_pack", self._lp(), zt.data_ptr(), yt.data_ptr(), self.z.data_ptr(),
+        self._call("ocx_dev_pack", self._lp(), zt.data_ptr(), yt.data_ptr(), self.z.data_ptr(),
                   self.y.data_ptr(), self._sp)
         self._keep = self._hold(zt, yt)
         return self
@@ -533,7 +540,7 @@ class DeviceBatch:
         if closed_comparator is None:
             closed_comparator = not self.exact and comparator is None
         flags = _lib.OCX_ALG_CLIPPED_ROWS if closed_comparator else 0
-        _lib.call("ocx_dev_simulate_alg_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        self._call("ocx_dev_simulate_alg_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   int(alg_flag), float(eta0), cp, self.regret.data_ptr(), self.cum.data_ptr(),
                   self.comp.data_ptr(), xp, flags,
                   closed_out.data_ptr() if closed_out is not None else None, self._sp)
@@ -561,7 +568,7 @@ class DeviceBatch:
             closed_comparator = not self.exact
         flags = ((_lib.OCX_SMART_CLOSED_PREFIX if closed_prefix else 0) |
                  (_lib.OCX_ALG_CLOSED_COMPARATOR if closed_comparator else 0))
-        _lib.call("ocx_dev_simulate_smart_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        self._call("ocx_dev_simulate_smart_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   th.data_ptr(), float(eta0), self.regret.data_ptr(), sp, flags,
                   stats.data_ptr() if stats is not None else None, self._sp)
         self._keep_th = self._hold(th)
@@ -577,7 +584,7 @@ class DeviceBatch:
             if int(algo) == 2:
                 th = torch.as_tensor(np.broadcast_to(np.asarray(thresh, dtype=np.float64),
                                                      (self.L.B,)).copy()).to(self.device)
-        _lib.call("ocx_dev_twin32", self._lp(), self.z.data_ptr(), self.y.data_ptr(), int(algo),
+        self._call("ocx_dev_twin32", self._lp(), self.z.data_ptr(), self.y.data_ptr(), int(algo),
                   float(eta0), th.data_ptr() if th is not None else None, res.data_ptr(), None,
                   None, None, self._sp)
         if th is not None:
@@ -593,7 +600,7 @@ class DeviceBatch:
         if regime is None:
             with self._on_stream():
                 regime = torch.zeros(max(self.L.B, 1), dtype=torch.int32, device=self.device)
-        _lib.call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        self._call("ocx_dev_ftl_exact", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   _norm_code(norm),
                   self.cum.data_ptr(), self.comp.data_ptr(),
                   cmp_action.data_ptr() if cmp_action is not None else None,
@@ -623,7 +630,7 @@ class DeviceBatch:
             # OCX_LANES_BEST: chained totals leave this kernel latency-bound (43 vs 28 ms at
             # 32768 x 1e4 x 64, profiles/r02_fused_exact_lanes.jsonl): butterfly sums instead
             flags |= _lib.OCX_ALG_TREE_SUMS
-        _lib.call("ocx_dev_ftrl_vs_exact_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
+        self._call("ocx_dev_ftrl_vs_exact_ex", self._lp(), self.z.data_ptr(), self.y.data_ptr(),
                   float(eta0), self.cum.data_ptr(), self.cum_exact.data_ptr(),
                   self.comp.data_ptr(), comp_ftl.data_ptr() if comp_ftl is not None else None,
                   cmp_action.data_ptr() if cmp_action is not None else None, regime.data_ptr(),
@@ -647,7 +654,7 @@ class DeviceBatch:
             for k in ("obj", "gap", "step_loss"):
                 out[k] = torch.zeros((max(B, 1), NP), dtype=torch.float64, device=self.device)
             out["info"] = torch.zeros((max(B, 1), NP), dtype=torch.int32, device=self.device)
-        _lib.call("ocx_dev_exact_ball_solve_tiled", self._lp(), self.z.data_ptr(),
+        self._call("ocx_dev_exact_ball_solve_tiled", self._lp(), self.z.data_ptr(),
                   self.y.data_ptr(), _norm_code(norm), int(bool(all_prefixes)),
                   out["actions"].data_ptr(), out["obj"].data_ptr(), out["gap"].data_ptr(),
                   out["step_loss"].data_ptr(), out["info"].data_ptr(), self._sp)
@@ -674,7 +681,7 @@ class DeviceBatch:
             for k in ("obj", "gap", "step_loss"):
                 res[k] = torch.zeros((nb, T + 1), dtype=torch.float64, device=self.device)
             res["info"] = torch.zeros((nb, T + 1), dtype=torch.int32, device=self.device)
-            _lib.call("ocx_dev_exact_ball_solve", zb.data_ptr(), yb.data_ptr(), nb, T, d,
+            self._call("ocx_dev_exact_ball_solve", zb.data_ptr(), yb.data_ptr(), nb, T, d,
                       _norm_code(norm), 1, res["actions"].data_ptr(), res["obj"].data_ptr(),
                       res["gap"].data_ptr(), res["step_loss"].data_ptr(),
                       res["info"].data_ptr(), self._sp)
@@ -715,7 +722,7 @@ class DeviceBatch:
         flags = 0 if pipelined else _lib.OCX_GENSIM_SEQUENTIAL
         if self.exact:
             flags |= _lib.OCX_GENSIM_TWO_PASS
-        _lib.call("ocx_dev_gen_simulate", self._lp(), int(base_seed), int(run0), int(nbatch),
+        self._call("ocx_dev_gen_simulate", self._lp(), int(base_seed), int(run0), int(nbatch),
                   self.z.data_ptr(), self.y.data_ptr(), float(eta0), self.regret.data_ptr(),
                   gmax.data_ptr() if gmax is not None else None, flags, int(sub_seqs), self._sp)
         self.rows_clipped = True
@@ -726,7 +733,7 @@ class DeviceBatch:
         if out is None:
             with self._on_stream():
                 out = torch.zeros(1, dtype=torch.float64, device=self.device)
-        _lib.call("ocx_dev_max_regret", self.regret.data_ptr(), int(self.L.B), out.data_ptr(),
+        self._call("ocx_dev_max_regret", self.regret.data_ptr(), int(self.L.B), out.data_ptr(),
                   self._sp)
         return out
 

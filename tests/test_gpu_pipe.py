@@ -101,58 +101,39 @@ def test_pipe_kernel_long_horizon_drift(eng):
         assert close(r[b], O.simulate_alg(zz, yy, 0, SQ2)), b
 
 
-@pytest.mark.parametrize("P,d", [(8, 64), (16, 64), (32, 1024)])
-def test_spec_step_is_bit_identical(eng, P, d, monkeypatch):
-    """The SPEC step (ĝ_{t-1} = −y_{t-1}/2 assumed, every step checked, a wave whose check
-    fails runs the plain loop again) against the plain pipelined step, OCX_PIPE_SPEC read per
-    launch: bit for bit on g(T) rows (no check fails) and on a batch whose checks fail in some
-    waves (a row outside the ball, labels other than ±1, exact ties on one-coordinate rows)."""
+@pytest.mark.parametrize("P,d,T,chunk", [(8, 64, 300, 64), (16, 64, 257, 128), (8, 128, 640, 192),
+                                         (32, 1024, 200, 64), (16, 512, 129, 64)])
+def test_chunked_pipe_is_bit_identical(eng, P, d, T, chunk):
+    """The pipelined kernel run in launches of `chunk` steps, its state carried through HBM
+    (the trailing pipeline's FTRL side, ocx_test_alg_pipe_chunked), against one launch:
+    bit-identical regrets for every sequence the closed form certifies; NaN and the bad flag
+    for the sequences it cannot (a row outside the ball, labels other than ±1), which a
+    chunked run cannot stream a second pass for."""
+    import ctypes
     import torch
-    B, T = 70, 300
-    rng = np.random.default_rng(P + d)
+    from online_convex_optimization_amd import _lib
+    B = 70
+    rng = np.random.default_rng(P + d + T)
     z = rng.standard_normal((B, T, d))
     z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
     y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
-    z[3] *= 1.7
+    z[3, T // 2] *= 1.7
     y[40, ::9] = 0.5
-    zf, yf, _ = O.flip_sequence(T, d=d)
-    z[60], y[60] = zf, yf
-    batches = [eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y),
-               eng.DeviceBatch(3 * 64 // P + 5, 2000, d, lanes_per_seq=P).generate_gT(7)]
-    for db in batches:
-        for flag in (0, 1):
-            out = {}
-            for spec in ("0", "1"):
-                monkeypatch.setenv("OCX_PIPE_SPEC", spec)
-                closed = torch.zeros(db.L.B, dtype=torch.int32, device=db.device)
-                r = db.simulate_alg(flag, SQ2, closed_comparator=True, closed_out=closed)
-                torch.cuda.synchronize()
-                out[spec] = (r[:db.L.B].cpu().numpy().copy(), db.cum[:db.L.B].cpu().numpy().copy(),
-                             closed[:db.L.B].cpu().numpy().copy())
-            for a, b in zip(out["0"], out["1"]):
-                assert np.array_equal(a, b), (P, d, flag)
-
-
-@pytest.mark.parametrize("T", [1, 2, 64, 65])
-def test_spec_step_short_horizons(eng, T, monkeypatch):
-    """SPEC at horizons around its pending-step bookkeeping (the step before step 0, the
-    last step finished after the loop, the 64-step refresh): bit for bit with the plain step
-    and within the bar of the C oracle."""
-    import torch
-    B, d, P = 24, 64, 8
-    rng = np.random.default_rng(T)
-    z = rng.standard_normal((B, T, d))
-    z /= np.maximum(1.0, np.linalg.norm(z, axis=2, keepdims=True))
-    y = np.where(rng.random((B, T)) < 0.5, -1.0, 1.0)
-    db = eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y)
-    for flag in (0, 1):
-        ref = O.simulate_alg_batch(z, y, flag, SQ2, nthreads=4)
-        out = {}
-        for spec in ("0", "1"):
-            monkeypatch.setenv("OCX_PIPE_SPEC", spec)
-            r = db.simulate_alg(flag, SQ2, closed_comparator=True)
-            torch.cuda.synchronize()
-            out[spec] = (r[:B].cpu().numpy().copy(), db.cum[:B].cpu().numpy().copy())
-        assert np.array_equal(out["0"][0], out["1"][0]) and np.array_equal(out["0"][1], out["1"][1])
-        assert close(out["1"][1], ref[1]), (T, flag)
-        assert close_closed(out["1"][0], ref[0], T), (T, flag)
+    packed = eng.DeviceBatch(B, T, d, lanes_per_seq=P).pack(z, y)
+    gen = eng.DeviceBatch(3 * 64 // P + 5, T, d, lanes_per_seq=P).generate_gT(7)
+    for db, unclean in ((packed, [3, 40]), (gen, [])):
+        assert (db.L.P, db.L.chain) == (P, 0)
+        n = db.L.B
+        whole = db.simulate_alg(0, SQ2, closed_comparator=True).clone()
+        got = torch.zeros(n, dtype=torch.float64, device=db.device)
+        bad = torch.zeros(1, dtype=torch.int32, device=db.device)
+        _lib.call("ocx_test_alg_pipe_chunked", ctypes.byref(db.L), db.z.data_ptr(),
+                  db.y.data_ptr(), SQ2, chunk, got.data_ptr(), bad.data_ptr(),
+                  db.stream.cuda_stream)
+        torch.cuda.synchronize()
+        w, g = whole[:n].cpu().numpy(), got.cpu().numpy()
+        ok = np.ones(n, dtype=bool)
+        ok[unclean] = False
+        assert np.array_equal(g[ok], w[ok]), (P, d, T, chunk)
+        assert np.all(np.isnan(g[~ok]))
+        assert int(bad.item()) == (1 if unclean else 0)

@@ -107,10 +107,11 @@ def test_generation_in_rounds_is_bit_identical(eng, monkeypatch):
 
 
 def test_pipeline_captures_into_a_graph(eng):
-    """ocx_dev_gen_simulate allocates nothing and never synchronises.  Under HIP graph capture
-    it stays on the capturing stream (sequential loop: the overlapped pipeline's fork to
-    library streams crashed HIP 7's capture), so a captured graph replays it with regrets and
-    g(T) equal to the eager, overlapped call's, bit for bit."""
+    """ocx_dev_gen_simulate allocates nothing and never synchronises, so the overlapped
+    pipeline — its fork to the library streams, the per-sub-batch events and the join back —
+    captures into a HIP graph, and the graph replays with regrets and g(T) equal to the eager
+    call's, bit for bit (every library stream waits on the fork event, and each
+    join has an event of its own)."""
     import torch
     B, T, d = 3000, 120, 64
     s = torch.cuda.Stream()
@@ -132,3 +133,55 @@ def test_pipeline_captures_into_a_graph(eng):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(db.regret[:B], ref) and float(gm.item()) == gref
+
+
+# ---- the trailing pipeline (ocx_run_gen_sim_trailing): capacity-limited resident batches
+# of ocx_gT_regrets / ocx_gT_max, batch k+1 generated chunk by chunk behind the chunked FTRL
+# pass over batch k in one z buffer.  A small OCX_HBM_BUDGET_GB makes the batches capacity-
+# limited at test sizes; OCX_TRAILING=0 is the sequential generate-then-simulate loop.
+
+def _capacity_limited(monkeypatch, gb):
+    monkeypatch.setenv("OCX_HBM_BUDGET_GB", str(gb))
+    monkeypatch.setenv("OCX_MIN_RESIDENT", "16")
+
+
+@pytest.mark.parametrize("T,d,runs,gb,chunks", [(2000, 64, 1000, 0.35, "8"), (700, 64, 900, 0.06, "3"),
+                                                (640, 1024, 130, 0.25, "4"), (300, 64, 500, 0.02, "2")])
+def test_trailing_equals_sequential(eng, monkeypatch, T, d, runs, gb, chunks):
+    """Regrets (host and device-resident) and g(T) of the trailing path equal the sequential
+    loop's bit for bit, over several batches and a smaller last one, and sampled sequences are
+    within the closed-form bar of the oracle."""
+    import torch
+    _capacity_limited(monkeypatch, gb)
+    monkeypatch.setenv("OCX_TRAIL_CHUNKS", chunks)
+    out = {}
+    for trail in ("0", "1"):
+        monkeypatch.setenv("OCX_TRAILING", trail)
+        reg = eng.gT_regrets(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
+        gm = eng.gT_max(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
+        dev = eng.gT_regrets_device(T, runs, base_seed=3, d=d, run0=11,
+                                    lanes_per_seq=eng.LANES_BEST)
+        torch.cuda.synchronize()
+        out[trail] = (reg, gm, dev.cpu().numpy())
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1] == eng.max_regret(out["0"][0])
+    assert np.array_equal(out["1"][2], out["0"][0])
+    for r in (0, runs // 2, runs - 1):
+        z, y = O.gT_sample(3, T, 11 + r, d)
+        assert close_closed(out["1"][0][r], O.simulate_alg(z, y, 0, SQ2), T), r
+
+
+def test_trailing_rerun_of_flagged_batches(eng, monkeypatch):
+    """A batch the trailing path flags (a sequence the closed form cannot certify: NaN regret)
+    runs again whole; the test hook flags every second batch, and the regrets stay the
+    sequential loop's bit for bit."""
+    from online_convex_optimization_amd import _lib
+    _capacity_limited(monkeypatch, 0.12)
+    T, d, runs = 1000, 64, 600
+    monkeypatch.setenv("OCX_TRAILING", "0")
+    ref = eng.gT_regrets(T, runs, base_seed=5, d=d, lanes_per_seq=eng.LANES_BEST)
+    monkeypatch.setenv("OCX_TRAILING", "1")
+    got = np.zeros(runs)
+    _lib.call("ocx_test_gT_regrets_unclean", 5, T, 0, runs, d, SQ2, _lib.ptr(got),
+              eng.LANES_BEST, 0, 2)
+    assert np.array_equal(got, ref)
