@@ -420,6 +420,48 @@ int64_t ocx_pipe_state_doubles(const ocx_layout* L) {
     return L->G * 64 * (int64_t)pipe_state_words(L->C);
 }
 
+// The lean form (ocx_pipeline.hip: the FTRL side of both pipelines): at most 128 VGPRs, so
+// one wave fits on a SIMD beside four generator waves of the 96-VGPR form (the sub-batch
+// pipeline) or four of the 80-VGPR few-stream form (the trailing pipeline); a shorter ring
+// (OCX_PIPE_LEAN_NB8 / _NB4 slots at 8 / 4 coordinates per lane) is what makes it fit.  FTRL
+// only, the pipelines' algorithm; 8 x 8 and 16 x 4 layouts.  One-wave blocks: the dispatcher
+// spreads them over the SIMDs the generator leaves room on.
+#ifndef OCX_PIPE_LEAN_NB8
+#define OCX_PIPE_LEAN_NB8 4
+#endif
+#ifndef OCX_PIPE_LEAN_NB4
+#define OCX_PIPE_LEAN_NB4 8
+#endif
+bool ocx_pipe_lean_supported(const ocx_layout* L) {
+    return !L->chain && L->T < ((int64_t)1 << 30) && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
+}
+
+namespace {
+hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
+    const dim3 grid = ocx_grid(a.gn, 1), block(64);
+    if (L->P == 8 && L->C == 8)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4>), grid, block, 0, st, a);
+    else if (L->P == 16 && L->C == 4)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
+                                    double eta0, double* reg, int onepass, int64_t g0,
+                                    int64_t gn, hipStream_t st) {
+    if (gn <= 0) return hipSuccess;
+    if (g0 < 0 || g0 + gn > L->G) return hipErrorInvalidValue;
+    PipeArgs a = pipe_args(L, zt, yt, eta0, reg, nullptr, nullptr, nullptr, onepass);
+    a.g0 = g0;
+    a.gn = gn;
+    return launch_lean(L, a, st);
+}
+
+// Chunked runs take the lean form where the layout has one (the trailing pipeline's
+// layouts: it runs beside the generator), the full form otherwise (tests of other layouts).
 hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                      double eta0, double* reg, int onepass, int64_t t0,
                                      int64_t tn, double* state, int* bad, hipStream_t st) {
@@ -432,37 +474,5 @@ hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, cons
     a.tn = tn;
     a.state = state;
     a.bad = bad;
-    return launch_pipe(L, a, 0, st);
-}
-
-// The lean form over wave-groups [g0, g0 + gn) (ocx_pipeline.hip): at most 128 VGPRs, so one
-// wave fits on a SIMD beside four generator waves of the 96-VGPR form; a shorter ring
-// (OCX_PIPE_LEAN_NB8 / _NB4 slots at 8 / 4 coordinates per lane) is what makes it fit.  FTRL
-// only, the pipeline's algorithm; 8 x 8 and 16 x 4 layouts.
-#ifndef OCX_PIPE_LEAN_NB8
-#define OCX_PIPE_LEAN_NB8 4
-#endif
-#ifndef OCX_PIPE_LEAN_NB4
-#define OCX_PIPE_LEAN_NB4 8
-#endif
-bool ocx_pipe_lean_supported(const ocx_layout* L) {
-    return !L->chain && L->T < ((int64_t)1 << 30) && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
-}
-
-hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
-                                    double eta0, double* reg, int onepass, int64_t g0,
-                                    int64_t gn, hipStream_t st) {
-    if (gn <= 0) return hipSuccess;
-    if (g0 < 0 || g0 + gn > L->G) return hipErrorInvalidValue;
-    PipeArgs a = pipe_args(L, zt, yt, eta0, reg, nullptr, nullptr, nullptr, onepass);
-    a.g0 = g0;
-    a.gn = gn;
-    const dim3 grid = ocx_grid(gn, 1), block(64);
-    if (L->P == 8 && L->C == 8)
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4>), grid, block, 0, st, a);
-    else if (L->P == 16 && L->C == 4)
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
+    return ocx_pipe_lean_supported(L) ? launch_lean(L, a, st) : launch_pipe(L, a, 0, st);
 }

@@ -532,7 +532,7 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
     // the reference's streamed pass (the bit-exact modes)
     const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
-    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) &&
+    if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) && ocx_stream_fork_ok(st) &&
         (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
                                           regret, onepass, acc ? fold_max : nullptr, acc,
@@ -1010,21 +1010,28 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         // loop below).  Its second label tile comes out of the budget.
         const char* te = std::getenv("OCX_TRAILING");
         bool trail = !pipe && onepass && (!te || std::atoi(te) != 0) &&
-                     ocx_trailing_supported(&Lp) && R / chunk >= 2;
+                     ocx_trailing_supported(&Lp) && R > chunk;
         if (trail) {
             const int64_t per_trail = per_seq + 8 * T + 64 * 8 * (2 * (int64_t)Lp.C + 7);
             int64_t c2 = std::max<int64_t>(64, std::min<int64_t>(budget / per_trail, R));
             const int64_t nb2 = (R + c2 - 1) / c2;
             c2 = (R + nb2 - 1) / nb2;
+            // and no more streams than fit beside the FTRL waves in one generator round
+            const int64_t cap = ocx_trailing_max_batch(&Lp);
+            if (c2 > cap) {
+                const int64_t nb3 = (R + cap - 1) / cap;
+                c2 = (R + nb3 - 1) / nb3;
+            }
             if (c2 < chunk) {
                 chunk = c2;
                 if (int rc = ocx_layout_init(chunk, T, d, lanes_per_seq, &Lp)) return rc;
                 OCX_HIP(cx->out.ensure((size_t)chunk * 8));
             }
-            trail = ocx_trailing_supported(&Lp) && R / chunk >= 2;
+            trail = ocx_trailing_supported(&Lp) && R > chunk;
         }
         if (trail) {
-            const int64_t nfull = R / chunk;
+            // every batch, the last one holding the remainder in the same tiles
+            const int64_t nfull = (R + chunk - 1) / chunk, last_B = R - (nfull - 1) * chunk;
             OCX_HIP(cx->zt.ensure((size_t)Lp.z_elems * 8));
             OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
             OCX_HIP(cx->yt2.ensure((size_t)Lp.y_elems * 8));
@@ -1041,7 +1048,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             OCX_HIP(ocx_run_gen_sim_trailing(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
                                              cx->yt.as<double>(), cx->yt2.as<double>(),
                                              cx->gst.as<uint64_t>(), cx->fst.as<double>(),
-                                             cx->bad.as<int>(), eta0, rdst,
+                                             cx->bad.as<int>(), eta0, rdst, last_B,
                                              dmax ? fold_max : nullptr, dmax, nch, st));
             // a batch with a sequence the closed-form comparator could not certify (its regret
             // NaN, never the max) runs again whole: the kernel streams its second pass
@@ -1053,19 +1060,20 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
                 for (int64_t k = 0; k < nfull; k += test_unclean_every) hb[(size_t)k] = 1;
             for (int64_t k = 0; k < nfull; ++k) {
                 if (!hb[(size_t)k]) continue;
-                OCX_HIP(ocx_launch_gen_gT(&Lp, base_seed, run0 + k * chunk, cx->zt.as<double>(),
+                ocx_layout Lk = Lp;  // the last batch: same tiles, last_B runs
+                if (k + 1 == nfull) Lk.B = last_B;
+                OCX_HIP(ocx_launch_gen_gT(&Lk, base_seed, run0 + k * chunk, cx->zt.as<double>(),
                                           cx->yt.as<double>(), st));
-                OCX_HIP(ocx_launch_alg(&Lp, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0,
+                OCX_HIP(ocx_launch_alg(&Lk, cx->zt.as<double>(), cx->yt.as<double>(), 0, eta0,
                                        nullptr, rdst + k * chunk, nullptr, nullptr, nullptr, st,
                                        nullptr, nullptr, onepass));
-                if (dmax) OCX_HIP(launch_max_fold(rdst + k * chunk, chunk, dmax, st));
+                if (dmax) OCX_HIP(launch_max_fold(rdst + k * chunk, Lk.B, dmax, st));
             }
             if (!dmax && !regrets_on_device) {
-                OCX_HIP(hipMemcpyAsync(regrets, rdst, (size_t)(nfull * chunk) * 8,
-                                       hipMemcpyDeviceToHost, st));
+                OCX_HIP(hipMemcpyAsync(regrets, rdst, (size_t)R * 8, hipMemcpyDeviceToHost, st));
                 OCX_HIP(hipStreamSynchronize(st));
             }
-            done = nfull * chunk;
+            done = R;
         }
         if (pipe && dmax) {
             const int64_t nfull = R / chunk;

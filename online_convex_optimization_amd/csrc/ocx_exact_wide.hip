@@ -14,6 +14,8 @@
 // Padded coordinates (d <= j < DP) carry x_j = 0, a unit diagonal and no barrier term, so
 // their steps are 0.  This is a compute kernel: ≈50–100 Newton passes over each prefix's
 // rows (from L2), bound by the VALU.
+#include <algorithm>
+
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
@@ -31,6 +33,12 @@ constexpr double kBreakdown = 1e8;
 constexpr int RC = 64;  // rows per staged chunk
 
 __device__ __forceinline__ double wsum(double v) { return ocx_seq_sum<64>(v); }
+
+// Lanes hand values to each other through LDS (staged rows, row weights, the system and its
+// factor): every publish is followed by a barrier.  The block is one wave, so s_barrier
+// costs little; it orders the LDS traffic for the compiler as the memory model requires,
+// instead of relying on the wave's lockstep.
+__device__ __forceinline__ void lds_sync() { __syncthreads(); }
 
 // element (i, j) of sequence b's rows: row-major z [B][T][d] or the tiled layout
 struct WideSrc {
@@ -54,8 +62,9 @@ struct WideSrc {
 
 template <int DP, int NORM>
 __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
-    WideSrc rs, int64_t B, int64_t NP, double* __restrict__ actions, double* __restrict__ obj_out,
-    double* __restrict__ gap_out, double* __restrict__ step_loss, int32_t* __restrict__ info_out) {
+    WideSrc rs, int64_t B, int64_t NP, int64_t p0, double* __restrict__ actions,
+    double* __restrict__ obj_out, double* __restrict__ gap_out, double* __restrict__ step_loss,
+    int32_t* __restrict__ info_out) {
     constexpr int BS = DP / 8;       // block edge per lane
     constexpr int LD = DP + 1;       // LDS row stride (odd: conflict-free columns and rows)
     extern __shared__ double lds[];
@@ -67,7 +76,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
     double* sc = vv + 64;            // Jacobi scales
 
     const int lane = threadIdx.x & 63;
-    const int64_t p = blockIdx.x;
+    const int64_t p = p0 + blockIdx.x;
     if (p >= B * NP) return;
     const int d = rs.d;
     const int64_t T = rs.T;
@@ -84,6 +93,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
 
     // Stage rows [c0, c0 + rows) into M (zero-padded to DP columns) and y into yv (lane r).
     auto stage = [&](int64_t c0, int rows, double& yv) {
+        lds_sync();  // the previous chunk's readers are done with M
         const int tot = rows * d;
         for (int f = lane; f < tot; f += 64) {
             const int r = f / d, j = f - r * d;
@@ -95,6 +105,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
                 M[r * LD + j] = 0.0;
             }
         yv = lane < rows ? rs.yat(b, c0 + lane) : 0.0;
+        lds_sync();
     };
     // row r's residual z_r·x − y_r (lane r), in _dot's order from −y
     auto residual = [&](int r, double yv) {
@@ -105,6 +116,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
 
     while (!conv && it < kMaxIter) {
         ++it;
+        lds_sync();  // the last pass's readers of xs are done
         xs[lane] = x;
         double Gj = 0.0;
         double H[BS][BS];
@@ -127,6 +139,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
             }
             gw[lane] = g1;
             hw[lane] = h1;
+            lds_sync();
             for (int r = 0; r < rows; ++r) {
                 Gj = __builtin_fma(gw[r], M[r * LD + (lane < DP ? lane : 0)], Gj);
                 double a1[BS], a2[BS];
@@ -187,6 +200,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
             xs[lane] = v;
             c1 = gam;
         }
+        lds_sync();  // vv, xs published; the last chunk's reads of M are done
         // H + diag(vv) + c1·xs xsᵀ into M (full matrix)
 #pragma unroll
         for (int i = 0; i < BS; ++i) {
@@ -200,27 +214,31 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
                 M[gi * LD + gk] = h;
             }
         }
+        lds_sync();
         // Jacobi scaling, then Cholesky (lane i owns row i)
         const int ri = lane < DP ? lane : DP - 1;
         const double dg = M[ri * LD + ri];
         const double sci = 1.0 / sqrt(dg > 0.0 ? dg : kPivotFloor);
         sc[lane] = sci;
+        lds_sync();
         if (lane < DP)
             for (int j = 0; j <= lane; ++j) M[lane * LD + j] *= sci * sc[j];
+        lds_sync();
         for (int k = 0; k < DP; ++k) {
             double s = M[k * LD + k];
             s = s > kPivotFloor ? s : kPivotFloor;
             const double l = sqrt(s), rd = 1.0 / l;
             double lik = 0.0;
+            if (lane > k && lane < DP) lik = M[lane * LD + k] * rd;
+            lds_sync();  // every lane has read row k's diagonal before lane k rewrites it
             if (lane == k) M[k * LD + k] = l;
-            if (lane > k && lane < DP) {
-                lik = M[lane * LD + k] * rd;
-                M[lane * LD + k] = lik;
-            }
+            if (lane > k && lane < DP) M[lane * LD + k] = lik;
+            lds_sync();  // column k of the factor published
             if (lane > k && lane < DP)
                 for (int j = k + 1; j <= lane; ++j)
                     M[lane * LD + j] = __builtin_fma(-lik, M[j * LD + k], M[lane * LD + j]);
         }
+        lds_sync();
         // L w = rhs·sc ; Lᵀ v = −w ; dx = v·sc
         double vcur = lane < DP ? rhs_g * sci : 0.0, w = 0.0;
         for (int k = 0; k < DP; ++k) {
@@ -277,6 +295,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
     }
 
     // ---- certificate (as ocx_exact_ball.hip): obj, dual bounds of λ_a = r/(2s) and λ_b
+    lds_sync();
     xs[lane] = x;
     double P = 0.0, Ya = 0.0, Yb = 0.0, Wa = 0.0, Wb = 0.0;
     for (int64_t c0 = 0; c0 < n; c0 += RC) {
@@ -295,6 +314,7 @@ __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
         }
         gw[lane] = la;
         hw[lane] = lb;
+        lds_sync();
         for (int r = 0; r < rows; ++r) {
             const double a = M[r * LD + (lane < DP ? lane : 0)];
             Wa = __builtin_fma(gw[r], a, Wa);
@@ -345,9 +365,16 @@ template <int DP, int NORM>
 hipError_t launch_wide_dn(const WideSrc& rs, int64_t B, int64_t NP, double* actions, double* obj,
                           double* gap, double* step_loss, int32_t* info, hipStream_t st) {
     const size_t lds = (size_t)(RC * (DP + 1) + 5 * 64) * sizeof(double);
-    hipLaunchKernelGGL((ocx_exact_wide_kernel<DP, NORM>), dim3((unsigned)(B * NP)), dim3(64), lds,
-                       st, rs, B, NP, actions, obj, gap, step_loss, info);
-    return hipGetLastError();
+    // one 64-thread block per problem, launched in slices: a launch may hold at most 2^32 - 1
+    // threads along x
+    const int64_t total = B * NP, slice = (int64_t)1 << 24;
+    for (int64_t p0 = 0; p0 < total; p0 += slice) {
+        hipLaunchKernelGGL((ocx_exact_wide_kernel<DP, NORM>), dim3((unsigned)std::min(slice, total - p0)),
+                           dim3(64), lds, st, rs, B, NP, p0, actions, obj, gap, step_loss, info);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 template <int DP>
@@ -371,7 +398,7 @@ hipError_t ocx_launch_exact_wide(const double* z, const double* y, int64_t B, in
                                  double* step_loss, int32_t* info, hipStream_t st) {
     const int64_t NP = all_prefixes ? T + 1 : 1;
     if (B == 0 || NP == 0) return hipSuccess;
-    if (d < 1 || d > 64 || B * NP > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (d < 1 || d > 64 || B > ((int64_t)1 << 40) / std::max<int64_t>(NP, 1)) return hipErrorInvalidValue;
     const WideSrc rs{z, y, T, G, (int)d, P, C, S, tiled};
     if (d <= 16) return launch_wide_d<16>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
     if (d <= 32) return launch_wide_d<32>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);

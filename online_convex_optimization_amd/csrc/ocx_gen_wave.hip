@@ -1573,9 +1573,11 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
     const int64_t nseq = L->G * L->S;
     if (nseq == 0 || L->T == 0) return hipSuccess;
     // d = 64 batches of four or more generator rounds: one round per launch over two streams
-    // (ocx_run_gen_rounds), bit-identical; OCX_GEN_ROUNDS=0 keeps the single launch (tuning)
+    // (ocx_run_gen_rounds), bit-identical; OCX_GEN_ROUNDS=0 keeps the single launch (tuning),
+    // and so does a stream whose capture cannot fork (ocx_stream_fork_ok)
     const char* gr = std::getenv("OCX_GEN_ROUNDS");
-    if ((!gr || std::atoi(gr) != 0) && ocx_pipeline_supported(L) && ocx_pipeline_worth(L, 4))
+    if ((!gr || std::atoi(gr) != 0) && ocx_pipeline_supported(L) && ocx_pipeline_worth(L, 4) &&
+        ocx_stream_fork_ok(st))
         return ocx_run_gen_rounds(L, base_seed, run0, zt, ytl, st);
     return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt,
                           ytl, nullptr, nullptr, nullptr, nullptr, st);

@@ -90,6 +90,22 @@ int64_t lcm64(int64_t a, int64_t b) {
 
 }  // namespace
 
+// Whether the multi-stream paths (the sub-batch pipeline, the generator rounds) may fork to
+// the library streams from `st`: always outside graph capture; under capture only on a HIP
+// runtime whose capture of a fork / join survives hipStreamEndCapture.  HIP 7.0 (the runtime
+// torch 2.10+rocm7.0 ships, which the package's processes load) segfaults there on a plain
+// three-stream fork / join with no library code at all (tools/capture_repro.hip stage 1 on
+// torch's libamdhip64: profiles/r05_capture_repro_torchhip.log; the same pattern in torch
+// alone, tools/capture_torch_repro.py, likewise), while ROCm 7.2's runtime captures it and
+// this library's overlapped pipeline bit for bit (stages 1-3, r05_capture_repro.log).  On
+// the older runtimes a captured call keeps to `st` (the sequential loop, same results).
+bool ocx_stream_fork_ok(hipStream_t st) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs == hipStreamCaptureStatusNone) return true;
+    int v = 0;
+    return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
+}
+
 bool ocx_pipeline_supported(const ocx_layout* L) {
     return L->d == 64 && L->P * L->C == 64 && ocx_pipe_lean_supported(L) && L->T > 0 &&
            L->T * L->d < ((int64_t)1 << 32);
@@ -257,19 +273,49 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 // fst: ocx_pipe_state_doubles(L); bad[nbatch]: set for a batch with a sequence the closed-form
 // comparator could not certify (its regret is NaN: the caller reruns that batch whole);
 // regret: nbatch·B doubles, batch k's at regret + k·B; fold(regret_k, B, fold_arg, stream)
-// after each batch (nullable).
+// after each batch (nullable).  The last batch may hold fewer runs (last_B <= B): it keeps the
+// layout's tiles, its spare sequences are padding.
+//
+// Registers decide where it pays.  The FTRL chunks run in the lean form (<= 128 VGPRs) beside
+// generator waves of the few-stream form (80 VGPRs: six per SIMD alone, four beside an FTRL
+// wave), so a batch is capped where every generator wave still fits beside the FTRL waves
+// (ocx_trailing_max_batch; 8 x 8 at d = 64: ≈4 900 streams).  d = 1024 has no such pairing: its
+// generator waves take 128 VGPRs and its FTRL waves (32 x 32) the whole 512-register file, so
+// a batch's generation and FTRL need ≈1.3 × the register file at once and cannot run side by
+// side (measured: 2.15e8 vs 2.20e8 timesteps/s sequential, profiles/r05_trail_probe.jsonl);
+// it keeps the sequential loop.
 bool ocx_trailing_supported(const ocx_layout* L) {
-    return ocx_pipe_supported(L) && L->T >= 128 && L->T * L->d < ((int64_t)1 << 32);
+    return ocx_pipe_lean_supported(L) && L->T >= 128 && L->T * L->d < ((int64_t)1 << 32);
+}
+
+int64_t ocx_trailing_max_batch(const ocx_layout* L) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const int64_t simds = 4 * (int64_t)cus, S = L->S;
+    // generator waves that fit: 4 on a SIMD beside an FTRL wave, 6 on one without
+    int64_t b = simds * 6;
+    while (b > S) {
+        const int64_t nf = std::min(simds, (b + S - 1) / S);
+        if (nf * 4 + (simds - nf) * 6 >= b) break;
+        b -= S;
+    }
+    return b;
 }
 
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,
-                                    double* regret,
+                                    double* regret, int64_t last_B,
                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
                                     void* fold_arg, int nchunks, hipStream_t st) {
-    if (!ocx_trailing_supported(L) || nbatch <= 0 || !regret || !gst || !fst || !bad)
+    if (!ocx_trailing_supported(L) || nbatch <= 0 || !regret || !gst || !fst || !bad ||
+        last_B < 1 || last_B > L->B)
         return hipErrorInvalidValue;
+    ocx_layout Ll = *L;  // the last batch: same tiles, last_B runs
+    Ll.B = last_B;
+    auto lay = [&](int64_t k) { return k + 1 == nbatch ? &Ll : L; };
     int dev = 0;
     OCX_PIPE_TRY(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
@@ -288,7 +334,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
     OCX_PIPE_TRY(hipMemsetAsync(bad, 0, (size_t)nbatch * sizeof(int), st));
     // batch 0 in one launch (the plain one: ocx_launch_gen_gT's rounds would take this lock);
     // the FTRL stream starts after it and after the caller's work
-    OCX_PIPE_TRY(ocx_launch_gen_gT_rows(L, base_seed, run0, 0, L->T, nullptr, nullptr, 1, zt, yt0, st));
+    OCX_PIPE_TRY(ocx_launch_gen_gT_rows(lay(0), base_seed, run0, 0, L->T, nullptr, nullptr, 1, zt, yt0, st));
     for (int64_t k = 0; k < nbatch; ++k) {
         // FTRL k: batch k is generated (its last launch was queued on st just before)
         OCX_PIPE_TRY(hipEventRecord(c.fork, st));
@@ -296,11 +342,11 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
         double* yk = yts[k & 1];
         for (int64_t ci = 0; ci < nch; ++ci) {
             const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
-            OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(L, zt, yk, eta0, regret + k * L->B, 1, t0, tn,
+            OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(lay(k), zt, yk, eta0, regret + k * L->B, 1, t0, tn,
                                                    fst, bad + k, F));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)ci], F));
         }
-        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, L->B, fold_arg, F));
+        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, lay(k)->B, fold_arg, F));
         if (k + 1 == nbatch) break;
         // batch k+1, chunk by chunk behind FTRL k; its labels with the last chunk
         const int64_t rk = run0 + (k + 1) * L->B;
@@ -308,7 +354,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
             const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
             const bool lastc = ci + 1 == nch;
             OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)ci], 0));
-            OCX_PIPE_TRY(ocx_launch_gen_gT_rows(L, base_seed, rk, t0, tn,
+            OCX_PIPE_TRY(ocx_launch_gen_gT_rows(lay(k + 1), base_seed, rk, t0, tn,
                                                 ci == 0 ? nullptr : gst + ((ci - 1) & 1) * words,
                                                 lastc ? nullptr : gst + (ci & 1) * words,
                                                 lastc ? 1 : 0, zt, yts[(k + 1) & 1], st));

@@ -43,6 +43,8 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
 // regret = the last batch's, fold(regret_sub, n, fold_arg, stream) after every sub-batch
 bool ocx_pipeline_supported(const ocx_layout* L);
 bool ocx_pipeline_worth(const ocx_layout* L, int wps);
+// the multi-stream paths may fork from st (not under graph capture on HIP runtimes < 7.2)
+bool ocx_stream_fork_ok(hipStream_t st);
 hipError_t ocx_launch_gen_gT_range_lr(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                       int64_t b_off, int64_t nseq, double* zt, double* ytl,
                                       hipStream_t st);
@@ -57,10 +59,12 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 // generation of batch k+1 trailing the chunked FTRL pass over batch k in one z buffer
 // (ocx_pipeline.hip: the capacity-limited batches); see there for the buffers
 bool ocx_trailing_supported(const ocx_layout* L);
+// the largest batch whose generator waves all fit beside the FTRL chunks' waves
+int64_t ocx_trailing_max_batch(const ocx_layout* L);
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,
-                                    double* regret,
+                                    double* regret, int64_t last_B,
                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
                                     void* fold_arg, int nchunks, hipStream_t st);
 // rows [t_off, t_off + nrows) of L's full-horizon tile, streams fresh (st_in null) or resumed

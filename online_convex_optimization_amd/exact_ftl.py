@@ -16,9 +16,15 @@ minimiser maximises x·S_t over the ball (engine.ftl_prefix_actions_batch / ftl_
 * linf ball (regime sum_j |z_tj| <= 1 — rows this small are rare in the reference's data):
   sign(S_t) componentwise.
 
-* Degenerate prefixes (S_t = 0, e.g. the empty prefix; ties in |S_j| for l1; zero
-  coordinates of S_t for linf): the maximiser is not unique and cvxpy's choice is
-  solver-dependent; the engine returns the point above (0 where S_t = 0).
+* Degenerate prefixes: where the maximiser is not unique the closed forms would pick one
+  vertex of the optimal face, while an interior-point solver (the ECOS / Clarabel backends
+  cvxpy picks) approaches the face's analytic centre.  So tied prefixes leave the closed
+  form (ocx_exact_poly_tie / the oracle's _poly_tie): for l1 two or more coordinates at the
+  largest |S_j| > 0, for linf a zero coordinate of S_t that a row of the prefix touched.
+  The general solver below answers those sequences (the analytic centre); for linf that
+  sends the flip / switching families, whose rows touch one coordinate at a time, to the
+  O(T^2) general path.  S_t = 0 (e.g. the empty prefix) keeps x = 0, which is that centre.
+  Which point of the face cvxpy itself returns is solver-dependent: parity unpinned.
 * Outside the regime (a row beyond the dual ball, a label other than ±1 — the linf ball on
   the reference's own rows) the GPU solves the SOCP / LP itself: a log-barrier path with a
   certified duality gap (engine.exact_ball_solve; d <= 64, larger d raises

@@ -107,11 +107,12 @@ def test_generation_in_rounds_is_bit_identical(eng, monkeypatch):
 
 
 def test_pipeline_captures_into_a_graph(eng):
-    """ocx_dev_gen_simulate allocates nothing and never synchronises, so the overlapped
-    pipeline — its fork to the library streams, the per-sub-batch events and the join back —
-    captures into a HIP graph, and the graph replays with regrets and g(T) equal to the eager
-    call's, bit for bit (every library stream waits on the fork event, and each
-    join has an event of its own)."""
+    """ocx_dev_gen_simulate allocates nothing and never synchronises.  Under HIP graph capture
+    on the HIP 7.0 runtime torch ships, which segfaults ending the capture of any three-stream
+    fork / join (tools/capture_repro.hip, tools/capture_torch_repro.py), it keeps
+    to the capturing stream (ocx_stream_fork_ok); on ROCm 7.2's runtime the overlapped
+    pipeline itself captures (the reproducer's stages 2-3).  Either way a captured graph
+    replays with regrets and g(T) equal to the eager, overlapped call's, bit for bit."""
     import torch
     B, T, d = 3000, 120, 64
     s = torch.cuda.Stream()
