@@ -91,8 +91,9 @@ struct PipeArgs {
 };
 
 // RT (FTRL): the rescale's sqrt only in waves where a sequence may need the rescale (see the
-// step).  MINW: waves per SIMD the register allocation must allow (launch bounds).
-template <int C, int P, int NB, bool FTL, bool RT>
+// step).  CHUNK: a chunked run (t0, tn, state); the whole-run kernels compile without it, so
+// its bookkeeping costs them no registers (the lean form spilled with it: 148 B per lane).
+template <int C, int P, int NB, bool FTL, bool RT, bool CHUNK = false>
 __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
     static_assert(P >= 2 && NB >= 4, "butterfly layouts, a ring holding z_{t-1} .. z_{t+1}");
     using IT = typename std::conditional<(C <= OCX_PIPE_IT32_MAXC), int, int64_t>::type;
@@ -105,8 +106,8 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
     const int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_pipe_wave_id(a.gn));
     if (wv >= a.gn) return;
     const int64_t g = a.g0 + wv;
-    const int64_t T = a.T, t0 = a.t0, tn = a.tn;
-    const bool first = t0 == 0, last = t0 + tn >= T;
+    const int64_t T = a.T, t0 = CHUNK ? a.t0 : 0, tn = CHUNK ? a.tn : T;
+    const bool first = !CHUNK || t0 == 0, last = !CHUNK || t0 + tn >= T;
     const double eta0 = a.eta0;
 #if OCX_PIPE_WAVE_CLOCK  // diagnostic build only: see the end of the body
     const uint64_t clk0 = __builtin_amdgcn_s_memrealtime();
@@ -125,7 +126,8 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
     const ocx_d2* __restrict__ zg = reinterpret_cast<const ocx_d2*>(a.zt) + (g * T + t0) * tstride;
     const int64_t kst = a.G * T * 64;  // plane stride (pairs k)
     const double* __restrict__ yg = a.yt + (g * T + t0) * S;
-    double* __restrict__ stw = a.state ? a.state + g * NS * 64 + lane : nullptr;
+    // word i of this lane's carried state (formed where used: nothing stays live over the loop)
+    auto stw = [&](int i) -> double& { return a.state[(g * NS + i) * 64 + lane]; };
 
     double th[C];  // θ_{t-1} (lagging one update)
     double gp = 0.0;                                   // g_{t-1}
@@ -143,18 +145,18 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
         for (int j = 0; j < C; ++j) th[j] = 0.0;
 #pragma unroll
         for (int k = 0; k < K; ++k) zb[NB - 1][k] = ocx_d2{0.0, 0.0};
-    } else {
+    } else if constexpr (CHUNK) {
 #pragma unroll
-        for (int j = 0; j < C; ++j) th[j] = stw[j * 64];
+        for (int j = 0; j < C; ++j) th[j] = stw(j);
 #pragma unroll
-        for (int k = 0; k < K; ++k) zb[NB - 1][k] = ocx_d2{stw[(C + 2 * k) * 64], stw[(C + 2 * k + 1) * 64]};
-        A = stw[(2 * C) * 64];
-        Bz = stw[(2 * C + 1) * 64];
-        V = stw[(2 * C + 2) * 64];
-        W = stw[(2 * C + 3) * 64];
-        gp = stw[(2 * C + 4) * 64];
-        cum = stw[(2 * C + 5) * 64];
-        clean = stw[(2 * C + 6) * 64] != 0.0;
+        for (int k = 0; k < K; ++k) zb[NB - 1][k] = ocx_d2{stw(C + 2 * k), stw(C + 2 * k + 1)};
+        A = stw(2 * C);
+        Bz = stw(2 * C + 1);
+        V = stw(2 * C + 2);
+        W = stw(2 * C + 3);
+        gp = stw(2 * C + 4);
+        cum = stw(2 * C + 5);
+        clean = stw(2 * C + 6) != 0.0;
     }
     auto load = [&](int slot, int64_t tl) {
         const ocx_d2* __restrict__ row = zg + tl * tstride;  // uniform
@@ -240,26 +242,26 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
         A = an;
         Bz = bn;
         gp = gq;
-    }, T - t0);
+    }, CHUNK ? T - t0 : T);
     // the chunk's last row: z_{t1-1} for the next chunk, or z_{T-1} for θ_T (loaded again:
     // its ring slot is not known at compile time)
     ocx_d2 zl[K];
     if (tn > 0) ocx_load_tile<C>(zl, zg + (tn - 1) * tstride + lane, kst);
-    if (!last) {
+    if constexpr (CHUNK) if (!last) {
 #pragma unroll
-        for (int j = 0; j < C; ++j) stw[j * 64] = th[j];
+        for (int j = 0; j < C; ++j) stw(j) = th[j];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            stw[(C + 2 * k) * 64] = zl[k].x;
-            stw[(C + 2 * k + 1) * 64] = zl[k].y;
+            stw(C + 2 * k) = zl[k].x;
+            stw(C + 2 * k + 1) = zl[k].y;
         }
-        stw[(2 * C) * 64] = A;
-        stw[(2 * C + 1) * 64] = Bz;
-        stw[(2 * C + 2) * 64] = V;
-        stw[(2 * C + 3) * 64] = W;
-        stw[(2 * C + 4) * 64] = gp;
-        stw[(2 * C + 5) * 64] = cum;
-        stw[(2 * C + 6) * 64] = clean ? 1.0 : 0.0;
+        stw(2 * C) = A;
+        stw(2 * C + 1) = Bz;
+        stw(2 * C + 2) = V;
+        stw(2 * C + 3) = W;
+        stw(2 * C + 4) = gp;
+        stw(2 * C + 5) = cum;
+        stw(2 * C + 6) = clean ? 1.0 : 0.0;
         return;
     }
     // θ_T = θ_{T-1} + g_{T-1} z_{T-1}
@@ -284,7 +286,7 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
                 const double qq = ocx_total<C, P, false>(p, lane);
                 comp += 0.5 * fabs(qq - yb[u]);
             });
-        } else {
+        } else if constexpr (CHUNK) {
             comp = __builtin_nan("");
             if (!closed && c == 0 && a.bad) *a.bad = 1;
         }
@@ -322,9 +324,9 @@ template <int C, int P, int MINW>
 constexpr bool pipe_rt() {
     return !(C == 8 && P == 8 && MINW == 1);
 }
-template <int C, int P, int NB, bool FTL, int MINW = 1>
+template <int C, int P, int NB, bool FTL, int MINW = 1, bool CHUNK = false>
 __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(PipeArgs a) {
-    alg_pipe_body<C, P, NB, FTL, pipe_rt<C, P, MINW>()>(a);
+    alg_pipe_body<C, P, NB, FTL, pipe_rt<C, P, MINW>(), CHUNK>(a);
 }
 
 namespace {
@@ -350,7 +352,9 @@ hipError_t launch_pipe_cp(const PipeArgs& a, int ftl, hipStream_t st) {
     constexpr int NB = pipe_nb<C>(P);
     const int bw = pipe_block_waves(a.gn);
     const dim3 grid = ocx_grid(a.gn, bw), block(64 * bw);
-    if (ftl)
+    if (a.state)  // a chunked run (FTRL: the trailing pipeline's algorithm)
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false, 1, true>), grid, block, 0, st, a);
+    else if (ftl)
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, true>), grid, block, 0, st, a);
     else
         hipLaunchKernelGGL((ocx_alg_pipe_kernel<C, P, NB, false>), grid, block, 0, st, a);
@@ -439,12 +443,19 @@ bool ocx_pipe_lean_supported(const ocx_layout* L) {
 namespace {
 hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
     const dim3 grid = ocx_grid(a.gn, 1), block(64);
-    if (L->P == 8 && L->C == 8)
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4>), grid, block, 0, st, a);
-    else if (L->P == 16 && L->C == 4)
-        hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
-    else
+    if (L->P == 8 && L->C == 8) {
+        if (a.state)
+            hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4>), grid, block, 0, st, a);
+    } else if (L->P == 16 && L->C == 4) {
+        if (a.state)
+            hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4, true>), grid, block, 0, st, a);
+        else
+            hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
+    } else {
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 }  // namespace

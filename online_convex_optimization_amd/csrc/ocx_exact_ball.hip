@@ -416,9 +416,9 @@ hipError_t launch_d(const RowSrc& rs, int64_t B, int64_t NP, int norm, double* a
     }
 }
 
-hipError_t launch(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_prefixes,
-                  double* actions, double* obj, double* gap, double* step_loss, int32_t* info,
-                  hipStream_t st) {
+hipError_t solve(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_prefixes,
+                 double* actions, double* obj, double* gap, double* step_loss, int32_t* info,
+                 hipStream_t st) {
     const int64_t NP = all_prefixes ? rs.T + 1 : 1;
     if (B == 0 || NP == 0) return hipSuccess;
     switch (d) {
@@ -433,6 +433,16 @@ hipError_t launch(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_pref
                                          norm, all_prefixes, actions, obj, gap, step_loss, info,
                                          st);
     }
+}
+
+// the solve, then its certificate polished (ocx_launch_exact_polish)
+hipError_t launch(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_prefixes,
+                  double* actions, double* obj, double* gap, double* step_loss, int32_t* info,
+                  hipStream_t st) {
+    const hipError_t e = solve(rs, B, d, norm, all_prefixes, actions, obj, gap, step_loss, info, st);
+    if (e != hipSuccess) return e;
+    return ocx_launch_exact_polish(rs.z, rs.y, B, rs.T, d, rs.tiled, rs.P, rs.C, rs.S, rs.G, norm,
+                                   all_prefixes, actions, obj, gap, step_loss, st);
 }
 
 }  // namespace

@@ -404,3 +404,356 @@ hipError_t ocx_launch_exact_wide(const double* z, const double* y, int64_t B, in
     if (d <= 32) return launch_wide_d<32>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
     return launch_wide_d<64>(rs, B, NP, norm, actions, obj, gap, step_loss, info, st);
 }
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// Certificate polish (both general solvers, d <= 64): the solver's x purified onto the face its
+// active constraints define, and a dual rebuilt from the KKT system there, so the gap
+// certifies the objective to rounding.
+//
+// The barrier path stops at μ_end = 1e-10: its x sits about μ_end/|slope| inside the optimal
+// face, and its multipliers λ_i = r_i/(2 s_i) are exact for the rows the optimum does not
+// interpolate (±½) but only as good as μ_end for the ones it does.  Where the optimum
+// interpolates rows (n > d real-valued rows: an LAD vertex; n < d rows fitted exactly) the
+// barrier certificate stayed near 1e-5 relative, and a zero-loss prefix kept ½Σ|r_i| ≈ 5e-8.
+// For each of seven threshold scales (the best is kept; every bound is valid):
+//   1. active set at x: rows with |r_i| <= τ_r (1 + |y_i|) (at most 63), and the ball's
+//      constraints that hold: l2 ||x|| = 1; linf |x_j| = 1 (those coordinates fixed at ±1);
+//      l1 ||x||_1 = 1 (the zero coordinates fixed at 0, the others keep their signs);
+//   2. primal purification: the least-change step δ (minimum norm over the free coordinates)
+//      that makes the active rows' residuals and the tight constraint (l2: linearised) hold
+//      exactly, x' = x + δ projected into the ball, kept only if ½Σ|r| does not grow;
+//   3. dual at x': λ_i = ½ sign(r_i) off the active set, and on it the least-squares solution
+//      of stationarity Σ_A λ_i z_i = −g − w (g the other rows' part, w in the ball's normal
+//      cone: l2 ν x, l1 ν sign(x) on the support, linf free on the fixed coordinates), clipped
+//      to [−½, ½]; D = −λ·y − ||Zᵀλ||_* (weak duality: a bound whatever the λ in the box).
+// If the best scale certifies a smaller gap than the solver's, x', its objective, the gap and
+// the prefix's step loss replace the solver's.  One wave per problem; the small systems by
+// the solver's LDS Cholesky.
+__device__ void polish_cholesky_solve(double* K, double* sc, int lane, double rhs, double& out) {
+    // K: [64][65] SPD (identity past the system), rhs on lane k; out = K⁻¹ rhs on lane k
+    constexpr int DP = 64, LD = 65;
+    const double dg = K[lane * LD + lane];
+    const double sci = 1.0 / sqrt(dg > 0.0 ? dg : kPivotFloor);
+    sc[lane] = sci;
+    lds_sync();
+    for (int j = 0; j <= lane; ++j) K[lane * LD + j] *= sci * sc[j];
+    lds_sync();
+    for (int k = 0; k < DP; ++k) {
+        double s = K[k * LD + k];
+        s = s > kPivotFloor ? s : kPivotFloor;
+        const double l = sqrt(s), rd = 1.0 / l;
+        double lik = 0.0;
+        if (lane > k) lik = K[lane * LD + k] * rd;
+        lds_sync();
+        if (lane == k) K[k * LD + k] = l;
+        if (lane > k) K[lane * LD + k] = lik;
+        lds_sync();
+        if (lane > k)
+            for (int j = k + 1; j <= lane; ++j)
+                K[lane * LD + j] = __builtin_fma(-lik, K[j * LD + k], K[lane * LD + j]);
+    }
+    lds_sync();
+    double vcur = rhs * sci, w = 0.0;
+    for (int k = 0; k < DP; ++k) {
+        const double wk = ocx_readlane(vcur, k) / K[k * LD + k];
+        if (lane == k) w = wk;
+        if (lane > k) vcur = __builtin_fma(-K[lane * LD + k], wk, vcur);
+    }
+    double vb = w, ck = 0.0;
+    for (int k = DP - 1; k >= 0; --k) {
+        const double dk = ocx_readlane(vb, k) / K[k * LD + k];
+        if (lane == k) ck = dk;
+        if (lane < k) vb = __builtin_fma(-K[k * LD + lane], dk, vb);
+    }
+    out = ck * sci;
+    lds_sync();
+}
+
+template <int NORM>
+__global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
+    WideSrc rs, int64_t B, int64_t NP, int64_t p0, double* __restrict__ actions,
+    double* __restrict__ obj, double* __restrict__ gap, double* __restrict__ step_loss) {
+    constexpr int DP = 64, LD = DP + 1, AM = 63;
+    extern __shared__ double lds[];
+    double* M = lds;             // [64][LD] the active rows (+ the cone row)
+    double* K = M + DP * LD;     // [64][LD] staged rows during passes; the small systems
+    double* xs = K + DP * LD;    // x, then x'
+    double* wv = xs + 64;        // per-row weights of a staged chunk
+    double* gs = wv + 64;        // g = Σ_{i∉A} λ_i z_i
+    double* em = gs + 64;        // 1.0 where coordinate j's stationarity equation holds
+    double* sc = em + 64;        // Jacobi scales / λ_A
+    double* ra = sc + 64;        // active rows' residuals at x, then their y
+    int* act = reinterpret_cast<int*>(ra + 64);  // active row indices
+
+    const int lane = threadIdx.x & 63;
+    const int64_t p = p0 + blockIdx.x;
+    if (p >= B * NP) return;
+    const int d = rs.d;
+    const int64_t T = rs.T;
+    const int64_t b = p % B;
+    const int64_t n = T - p / B;
+    const int64_t o = b * NP + (NP == 1 ? 0 : n);
+    const double g0 = gap[o], f0 = obj[o];
+    if (n == 0 || !(g0 > 0.0)) return;  // exact already (or a NaN the caller reports)
+    const bool cj = lane < d;
+    const double x = cj ? actions[o * d + lane] : 0.0;
+    double best = g0, pbest = f0, xbest = x;
+    bool improved = false;
+
+    // stage rows [c0, c0 + rows) into K; y into yv (lane r)
+    auto stage = [&](int64_t c0, int rows, double& yv) {
+        lds_sync();
+        for (int f = lane; f < rows * d; f += 64) {
+            const int r = f / d, j = f - r * d;
+            K[r * LD + j] = rs.zat(b, c0 + r, j);
+        }
+        yv = lane < rows ? rs.yat(b, c0 + lane) : 0.0;
+        lds_sync();
+    };
+    auto resid = [&](int r, double yv) {  // staged row r at xs, in _dot's order from −y
+        double rr = -yv;
+        for (int j = 0; j < d; ++j) rr = __builtin_fma(K[r * LD + j], xs[j], rr);
+        return rr;
+    };
+
+    for (int sweep = 0; sweep < 7; ++sweep) {
+        const double tsc = sweep == 0 ? 1.0 : (sweep == 1 ? 1e3 : (sweep == 2 ? 1e2 : (sweep == 3 ? 10.0 :
+                           (sweep == 4 ? 1e4 : (sweep == 5 ? 0.1 : 0.01)))));
+        const double kTight = 1e-8 * tsc, kZero = 1e-7 * tsc;
+        // ---- 1. the ball's constraints at x
+        bool cone = false, fixed = false;
+        double tgt = 0.0, crow = 0.0;  // fixed coordinate's value; the cone row's entry
+        if constexpr (NORM == 0) {
+            cone = wsum(x * x) >= 1.0 - kTight;
+            crow = 2.0 * x;
+        } else if constexpr (NORM == 2) {
+            fixed = cj && fabs(x) >= 1.0 - kTight;
+            tgt = x > 0.0 ? 1.0 : -1.0;
+        } else {
+            cone = wsum(fabs(x)) >= 1.0 - kTight;
+            if (cone) {
+                fixed = cj && fabs(x) <= kZero;
+                tgt = 0.0;
+                crow = (cj && !fixed) ? (x > 0.0 ? 1.0 : -1.0) : 0.0;
+            }
+        }
+        const bool freec = cj && !fixed;
+        const double vfix = fixed ? tgt - x : 0.0;  // δ_j on a fixed coordinate
+        lds_sync();
+        xs[lane] = x;
+        em[lane] = freec ? 1.0 : 0.0;  // stationarity holds on the free coordinates
+        // ---- pass 1 at x: ½Σ|r|, the active set and its residuals
+        double P0 = 0.0;
+        int m = 0;
+        bool over = false;
+        for (int64_t c0 = 0; c0 < n; c0 += RC) {
+            const int rows = (int)(n - c0 < RC ? n - c0 : RC);
+            double yv;
+            stage(c0, rows, yv);
+            bool a = false;
+            double rr = 0.0;
+            if (lane < rows) {
+                rr = resid(lane, yv);
+                P0 += 0.5 * fabs(rr);
+                a = fabs(rr) <= kZero * (1.0 + fabs(yv));
+            }
+            const uint64_t am = __ballot(a);
+            const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+            if (a && m + pos < AM) {
+                act[m + pos] = (int)(c0 + lane);
+                ra[m + pos] = rr;
+            }
+            m += __builtin_popcountll(am);
+            over = over || m > AM;
+        }
+        if (over) continue;  // wave-uniform: too many active rows at this scale
+        P0 = wsum(P0);
+        const int mr = m + (cone ? 1 : 0);
+        lds_sync();
+        // ---- 2. primal purification: rows of the active set (+ the cone row) into M
+        for (int f = lane; f < m * d; f += 64) {
+            const int k = f / d, j = f - k * d;
+            M[k * LD + j] = rs.zat(b, act[k], j);
+        }
+        if (cone) M[m * LD + lane] = cj ? crow : 0.0;
+        sc[lane] = vfix;
+        lds_sync();
+        // right-hand sides: −r_k minus the fixed coordinates' part; the cone row's defect
+        double rhs = 0.0;
+        if (lane < m) {
+            rhs = -ra[lane];
+            for (int j = 0; j < d; ++j) rhs = __builtin_fma(-M[lane * LD + j], sc[j], rhs);
+        }
+        double defect;
+        if constexpr (NORM == 0) defect = 1.0 - wsum(x * x);
+        else defect = 1.0 - wsum(freec ? fabs(x) : 0.0);
+        if (cone && lane == m) rhs = defect;
+        // K = R_F R_Fᵀ over the free coordinates (+ ridge), identity past mr
+        if (lane < mr)
+            for (int l = 0; l < mr; ++l) {
+                double s2 = 0.0;
+                for (int j = 0; j < d; ++j) s2 = __builtin_fma(em[j] * M[lane * LD + j], M[l * LD + j], s2);
+                K[lane * LD + l] = s2;
+            }
+        for (int l = (lane < mr ? mr : 0); l < DP; ++l) K[lane * LD + l] = (l == lane) ? 1.0 : 0.0;
+        lds_sync();
+        const double trK = wsum(lane < mr ? K[lane * LD + lane] : 0.0);
+        if (lane < mr) K[lane * LD + lane] += 1e-13 * (trK / (mr > 0 ? mr : 1)) + 1e-300;
+        lds_sync();
+        double u = 0.0;
+        polish_cholesky_solve(K, sc, lane, lane < mr ? rhs : 0.0, u);
+        sc[lane] = lane < mr ? u : 0.0;
+        lds_sync();
+        double xn = x;
+        if (cj) {
+            if (fixed) {
+                xn = tgt;
+            } else {
+                double dl = 0.0;
+                for (int k = 0; k < mr; ++k) dl = __builtin_fma(M[k * LD + lane], sc[k], dl);
+                xn = x + dl;
+            }
+        }
+        // into the ball
+        if constexpr (NORM == 0) {
+            const double nn = sqrt(wsum(xn * xn));
+            if (nn > 1.0) xn = xn / nn;
+        } else if constexpr (NORM == 2) {
+            xn = fmin(fmax(xn, -1.0), 1.0);
+        } else {
+            const double s1 = wsum(fabs(xn));
+            if (s1 > 1.0) xn = xn / s1;
+        }
+        lds_sync();
+        xs[lane] = xn;
+        gs[lane] = 0.0;
+        // ---- pass 2 at x': ½Σ|r'|, λ_i = ½ sign(r'_i) off the active set into g and λ·y
+        double P1 = 0.0, Y = 0.0, gj = 0.0;
+        int ia = 0;  // next entry of act[] (the active rows come in increasing order)
+        for (int64_t c0 = 0; c0 < n; c0 += RC) {
+            const int rows = (int)(n - c0 < RC ? n - c0 : RC);
+            double yv;
+            stage(c0, rows, yv);
+            double lam = 0.0;
+            bool isact = false;
+            if (lane < rows) {
+                const double rr = resid(lane, yv);
+                P1 += 0.5 * fabs(rr);
+                // membership of row c0 + lane in act[ia ..) (sorted)
+                for (int k = ia; k < m && act[k] <= (int)(c0 + lane); ++k)
+                    if (act[k] == (int)(c0 + lane)) isact = true;
+                lam = isact ? 0.0 : (rr > 0.0 ? 0.5 : (rr < 0.0 ? -0.5 : 0.0));
+                Y = __builtin_fma(lam, yv, Y);
+            }
+            while (ia < m && act[ia] < (int)(c0 + rows)) ++ia;
+            wv[lane] = lam;
+            lds_sync();
+            if (cj)
+                for (int r = 0; r < rows; ++r) gj = __builtin_fma(wv[r], K[r * LD + lane], gj);
+        }
+        P1 = wsum(P1);
+        Y = wsum(Y);
+        if (!(P1 <= P0)) continue;  // the purified point is no better: keep x's certificate
+        lds_sync();
+        gs[lane] = gj;
+        if (lane < m) ra[lane] = rs.yat(b, act[lane]);
+        lds_sync();
+        // ---- 3. dual: least squares for λ_A (and ν) on the free coordinates' equations
+        double hk = 0.0;
+        if (lane < mr)
+            for (int j = 0; j < d; ++j) hk = __builtin_fma(em[j] * M[lane * LD + j], gs[j], hk);
+        if (lane < mr)
+            for (int l = 0; l < mr; ++l) {
+                double s2 = 0.0;
+                for (int j = 0; j < d; ++j) s2 = __builtin_fma(em[j] * M[lane * LD + j], M[l * LD + j], s2);
+                K[lane * LD + l] = s2;
+            }
+        for (int l = (lane < mr ? mr : 0); l < DP; ++l) K[lane * LD + l] = (l == lane) ? 1.0 : 0.0;
+        lds_sync();
+        const double trG = wsum(lane < mr ? K[lane * LD + lane] : 0.0);
+        if (lane < mr) K[lane * LD + lane] += 1e-13 * (trG / (mr > 0 ? mr : 1)) + 1e-300;
+        lds_sync();
+        double c = 0.0;
+        polish_cholesky_solve(K, sc, lane, lane < mr ? -hk : 0.0, c);
+        const double la = lane < m ? fmin(fmax(c, -0.5), 0.5) : 0.0;
+        Y += wsum(lane < m ? la * ra[lane] : 0.0);
+        sc[lane] = la;
+        lds_sync();
+        double wj = gj;
+        if (cj)
+            for (int k = 0; k < m; ++k) wj = __builtin_fma(sc[k], M[k * LD + lane], wj);
+        if (!cj) wj = 0.0;
+        double nw;
+        if constexpr (NORM == 0) {
+            nw = sqrt(wsum(wj * wj));
+        } else if constexpr (NORM == 2) {
+            nw = wsum(fabs(wj));
+        } else {
+            double mx = fabs(wj);
+            for (int s2 = 32; s2 > 0; s2 >>= 1) mx = fmax(mx, __shfl_xor(mx, s2, 64));
+            nw = mx;
+        }
+        const double gn = fmax(P1 - (-Y - nw), 0.0);
+        if (gn < best) {
+            best = gn;
+            pbest = P1;
+            xbest = xn;
+            improved = true;
+        }
+        if (best <= 1e-14 * (1.0 + pbest)) break;  // to rounding: done
+    }
+    if (!improved) return;
+    if (cj) actions[o * d + lane] = xbest;
+    lds_sync();
+    xs[lane] = xbest;
+    lds_sync();
+    if (lane == 0) {
+        obj[o] = pbest;
+        gap[o] = best;
+        if (step_loss && NP > 1) {
+            // FTL's loss at step n with this action (replay_exact_ftl :318-323: _dot's order)
+            double lo = 0.0;
+            if (n < T) {
+                double q = 0.0;
+                for (int j = 0; j < d; ++j) q = q + rs.zat(b, n, j) * xs[j];
+                lo = 0.5 * fabs(q - rs.yat(b, n));
+            }
+            step_loss[o] = lo;
+        }
+    }
+}
+
+template <int NORM>
+hipError_t launch_polish_n(const WideSrc& rs, int64_t B, int64_t NP, double* actions, double* obj,
+                           double* gap, double* step_loss, hipStream_t st) {
+    const size_t lds = (size_t)(2 * 64 * 65 + 7 * 64) * sizeof(double) + 64 * sizeof(int);
+    const int64_t total = B * NP, slice = (int64_t)1 << 24;
+    for (int64_t p0 = 0; p0 < total; p0 += slice) {
+        hipLaunchKernelGGL((ocx_exact_polish_kernel<NORM>), dim3((unsigned)std::min(slice, total - p0)),
+                           dim3(64), lds, st, rs, B, NP, p0, actions, obj, gap, step_loss);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t ocx_launch_exact_polish(const double* z, const double* y, int64_t B, int64_t T,
+                                   int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
+                                   int all_prefixes, double* actions, double* obj, double* gap,
+                                   double* step_loss, hipStream_t st) {
+    const int64_t NP = all_prefixes ? T + 1 : 1;
+    if (B == 0 || NP == 0 || !gap || !obj || !actions) return hipSuccess;
+    if (d < 1 || d > 64) return hipErrorInvalidValue;
+    const WideSrc rs{z, y, T, G, (int)d, P, C, S, tiled};
+    switch (norm) {
+        case 0: return launch_polish_n<0>(rs, B, NP, actions, obj, gap, step_loss, st);
+        case 1: return launch_polish_n<1>(rs, B, NP, actions, obj, gap, step_loss, st);
+        case 2: return launch_polish_n<2>(rs, B, NP, actions, obj, gap, step_loss, st);
+        default: return hipErrorInvalidValue;
+    }
+}

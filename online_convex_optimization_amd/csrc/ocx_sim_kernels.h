@@ -79,6 +79,13 @@ hipError_t ocx_launch_exact_wide(const double* z, const double* y, int64_t B, in
                                  int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
                                  int all_prefixes, double* actions, double* obj, double* gap,
                                  double* step_loss, int32_t* info, hipStream_t st);
+// the general solvers' certificate polish (ocx_exact_wide.hip): the actions purified onto
+// their active face and a dual rebuilt from the KKT system there; where that certifies a
+// smaller gap, actions, obj, gap and step_loss are replaced.  d <= 64
+hipError_t ocx_launch_exact_polish(const double* z, const double* y, int64_t B, int64_t T,
+                                   int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
+                                   int all_prefixes, double* actions, double* obj, double* gap,
+                                   double* step_loss, hipStream_t st);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

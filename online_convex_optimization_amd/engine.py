@@ -145,12 +145,13 @@ def exact_ball_solve(z, y, *, norm: str = "l2", all_prefixes: bool = True, devic
 
 
 # A general solve is accepted iff info >= 0 and gap <= EXACT_GAP_RTOL * (1 + |obj|).  The gap
-# is a dual bound built from the barrier's multipliers; where the optimum interpolates rows
-# exactly (n > d, real-valued rows) those multipliers are only as good as the residuals at
-# μ_end = 1e-10, so the certificate stays near 1e-5 relative while the objective itself is
-# accurate to ~1e-10 (a path run on to μ = 1e-13 moves it by 3e-10).  1e-4
-# passes those and still rejects a solve the step cap or a breakdown left far from optimal.
-EXACT_GAP_RTOL = 1e-4
+# comes from the better of two duals: the barrier's multipliers (exact for the rows the optimum
+# does not interpolate, only as good as μ_end = 1e-10 for the ones it does) and the dual the
+# certificate polish rebuilds from the KKT system at the solver's x (ocx_exact_polish_kernel:
+# ±½ on the first kind, least squares on stationarity for the second), which certifies the
+# objective to the primal's own accuracy (~1e-10) where the optimum interpolates rows (n > d,
+# real-valued rows: the barrier's certificate alone stayed near 1e-5 there).
+EXACT_GAP_RTOL = 1e-8
 
 
 def check_certificates(obj, gap, info, what: str = "exact FTL") -> float:
