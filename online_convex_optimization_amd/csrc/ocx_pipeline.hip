@@ -340,18 +340,15 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
         OCX_PIPE_TRY(hipEventRecord(c.fork, st));
         OCX_PIPE_TRY(hipStreamWaitEvent(F, c.fork, 0));
         double* yk = yts[k & 1];
+        const bool next = k + 1 < nbatch;
+        const int64_t rk = run0 + (k + 1) * L->B;
         for (int64_t ci = 0; ci < nch; ++ci) {
             const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
             OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(lay(k), zt, yk, eta0, regret + k * L->B, 1, t0, tn,
                                                    fst, bad + k, F));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)ci], F));
-        }
-        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, lay(k)->B, fold_arg, F));
-        if (k + 1 == nbatch) break;
-        // batch k+1, chunk by chunk behind FTRL k; its labels with the last chunk
-        const int64_t rk = run0 + (k + 1) * L->B;
-        for (int64_t ci = 0; ci < nch; ++ci) {
-            const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
+            if (!next) continue;
+            // batch k+1's chunk ci, behind FTRL k's; its labels with the last chunk
             const bool lastc = ci + 1 == nch;
             OCX_PIPE_TRY(hipStreamWaitEvent(st, c.ev_sim[(size_t)ci], 0));
             OCX_PIPE_TRY(ocx_launch_gen_gT_rows(lay(k + 1), base_seed, rk, t0, tn,
@@ -359,6 +356,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
                                                 lastc ? nullptr : gst + (ci & 1) * words,
                                                 lastc ? 1 : 0, zt, yts[(k + 1) & 1], st));
         }
+        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, lay(k)->B, fold_arg, F));
     }
     OCX_PIPE_TRY(hipEventRecord(c.join_sim, F));
     OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim, 0));

@@ -23,7 +23,7 @@ CASES = {"c4": (10000, 1024), "t1e5": (100000, 64)}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="c4,t1e5")
-    ap.add_argument("--chunks", default="8")
+    ap.add_argument("--chunks", default="12")
     ap.add_argument("--runs-c4", type=int, default=32768)
     ap.add_argument("--runs-t5", type=int, default=131072)
     ap.add_argument("--check", type=int, default=1, help="compare regrets with the sequential loop")
