@@ -88,6 +88,7 @@ struct PipeArgs {
     int64_t t0, tn;  // steps [t0, t0 + tn) (a whole run: 0, T)
     double* state;   // chunked runs: the carried state (nullable: whole run)
     int* bad;        // chunked runs: set when a sequence needs the second pass
+    unsigned long long* gmax;  // nullable: g(T) = max(0, max regret) folded in (bit pattern)
 };
 
 // RT (FTRL): the rescale's sqrt only in waves where a sequence may need the rescale (see the
@@ -298,6 +299,21 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
         const double nrm = sqrt(ocx_total<C, P, false>(p, lane));
         if (closed) comp = 0.5 * (double)T - nrm;
     }
+    // g(T) folded in here (the pipelines' FTRL launches): a max over the wave's sequences,
+    // then one 64-bit atomic max of the bit pattern per wave — positive doubles order as
+    // their bits, every candidate that can win is > +0.0 and a NaN never passes `>`, so this
+    // is ocx_max_fold_kernel's selection, bit-identical to the host's loop, without a
+    // separate launch that would wait for a free slot beside the generator (2-3 ms each).
+    if (a.gmax && __ballot(live) != 0) {  // wave-uniform
+        const double rg = cum - comp;
+        double mv = (c == 0 && live && rg > 0.0) ? rg : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double u = __shfl_xor(mv, o, 64);
+            if (u > mv) mv = u;
+        }
+        if (lane == 0 && mv > 0.0) atomicMax(a.gmax, (unsigned long long)__double_as_longlong(mv));
+    }
     if (c == 0 && live) {
         if (a.regret) a.regret[b] = cum - comp;
 #if OCX_PIPE_WAVE_CLOCK
@@ -462,12 +478,13 @@ hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
 
 hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
                                     double eta0, double* reg, int onepass, int64_t g0,
-                                    int64_t gn, hipStream_t st) {
+                                    int64_t gn, unsigned long long* gmax, hipStream_t st) {
     if (gn <= 0) return hipSuccess;
     if (g0 < 0 || g0 + gn > L->G) return hipErrorInvalidValue;
     PipeArgs a = pipe_args(L, zt, yt, eta0, reg, nullptr, nullptr, nullptr, onepass);
     a.g0 = g0;
     a.gn = gn;
+    a.gmax = gmax;
     return launch_lean(L, a, st);
 }
 
@@ -475,7 +492,8 @@ hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const
 // layouts: it runs beside the generator), the full form otherwise (tests of other layouts).
 hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                      double eta0, double* reg, int onepass, int64_t t0,
-                                     int64_t tn, double* state, int* bad, hipStream_t st) {
+                                     int64_t tn, double* state, int* bad,
+                                     unsigned long long* gmax, hipStream_t st) {
     if (L->G == 0 || tn <= 0) return hipSuccess;
     // onepass only: a chunk after the first cannot stream the second comparator pass
     if (t0 < 0 || t0 % 64 != 0 || t0 + tn > L->T || !state || !onepass || !ocx_pipe_supported(L))
@@ -485,5 +503,6 @@ hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, cons
     a.tn = tn;
     a.state = state;
     a.bad = bad;
+    a.gmax = t0 + tn >= L->T ? gmax : nullptr;  // the chunk that writes the regrets
     return ocx_pipe_lean_supported(L) ? launch_lean(L, a, st) : launch_pipe(L, a, 0, st);
 }

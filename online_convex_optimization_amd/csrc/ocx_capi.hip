@@ -496,9 +496,6 @@ int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* str
 }  // extern "C"
 
 namespace {
-hipError_t fold_max(const double* r, int64_t n, void* acc, hipStream_t st) {
-    return launch_max_fold(r, n, static_cast<unsigned long long*>(acc), st);
-}
 
 // ocx_pipeline.hip's knob (tuning; the default is the measured best): generator waves per
 // SIMD beside the FTRL kernel
@@ -535,7 +532,7 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) && ocx_stream_fork_ok(st) &&
         (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
-                                          regret, onepass, acc ? fold_max : nullptr, acc,
+                                          regret, onepass, acc,
                                           pipe_wps(), sub_seqs, st));
         return OCX_OK;
     }
@@ -1053,7 +1050,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
                                              cx->yt.as<double>(), cx->yt2.as<double>(),
                                              cx->gst.as<uint64_t>(), cx->fst.as<double>(),
                                              cx->bad.as<int>(), eta0, rdst, last_B,
-                                             dmax ? fold_max : nullptr, dmax, nch, st));
+                                             dmax, nch, st));
             // a batch with a sequence the closed-form comparator could not certify (its regret
             // NaN, never the max) runs again whole: the kernel streams its second pass
             std::vector<int> hb((size_t)nfull, 0);
@@ -1085,7 +1082,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
             OCX_HIP(ocx_run_gen_sim_pipelined(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
                                               cx->yt.as<double>(), eta0, cx->out.as<double>(),
-                                              onepass, fold_max, dmax, pipe_wps(), 0, st));
+                                              onepass, dmax, pipe_wps(), 0, st));
             done = nfull * chunk;
         }
         for (int64_t r0 = done; r0 < R; r0 += chunk) {
@@ -1098,7 +1095,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             if (pipe && ocx_pipeline_supported(&L) && ocx_pipeline_worth(&L, pipe_wps())) {
                 OCX_HIP(ocx_run_gen_sim_pipelined(&L, base_seed, run0 + r0, 1, cx->zt.as<double>(),
                                                   cx->yt.as<double>(), eta0, rdst, onepass,
-                                                  nullptr, nullptr, pipe_wps(), 0, st));
+                                                  nullptr, pipe_wps(), 0, st));
             } else {
                 OCX_HIP(ocx_launch_gen_gT(&L, base_seed, run0 + r0, cx->zt.as<double>(),
                                           cx->yt.as<double>(), st));
@@ -1226,7 +1223,7 @@ int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const 
     hipError_t e = hipSuccess;
     for (int64_t t0 = 0; t0 < L->T && e == hipSuccess; t0 += chunk_steps)
         e = ocx_launch_alg_pipe_chunk(L, z_tiled, y_tiled, eta0, regret, 1, t0,
-                                      std::min(chunk_steps, L->T - t0), state, bad, st);
+                                      std::min(chunk_steps, L->T - t0), state, bad, nullptr, st);
     const hipError_t es = hipStreamSynchronize(st);
     (void)hipFree(state);
     OCX_HIP(e);

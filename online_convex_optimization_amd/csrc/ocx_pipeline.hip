@@ -164,15 +164,14 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
 }
 
 // nbatch batches of L->B runs each (runs run0 + k·B, k < nbatch) through one z/y buffer of
-// layout L; regret[] holds the last batch's regrets, dmax (nullable, device) folds the max
-// over all of them (ocx_max_fold: bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
+// layout L; regret[] holds the last batch's regrets, gmax (nullable, device) folds the max
+// over all of them in the FTRL kernel (bit pattern of g(T) = max(0, max regret)).  sub_seqs <= 0:
 // one generator round per sub-batch (up to four below T = 1000).  Returns with the work queued
 // on `st` (joined).
 hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                      int64_t nbatch, double* zt, double* yt, double eta0,
-                                     double* regret, int onepass,
-                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
-                                     void* fold_arg, int wps, int64_t sub_seqs, hipStream_t st) {
+                                     double* regret, int onepass, unsigned long long* gmax,
+                                     int wps, int64_t sub_seqs, hipStream_t st) {
     if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
     int dev = 0, cus = 256;
     OCX_PIPE_TRY(hipGetDevice(&dev));
@@ -237,9 +236,8 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], gs));
             OCX_PIPE_TRY(hipStreamWaitEvent(ss, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
-                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S, ss));
-            const int64_t nreal = std::min(nb, L->B - b0);
-            if (fold && nreal > 0) OCX_PIPE_TRY(fold(regret + b0, nreal, fold_arg, ss));
+                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
+                                                      gmax, ss));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], ss));
             c.sim_recorded[(size_t)i] = 1;
         }
@@ -272,8 +270,8 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 // z, y[2]: the layout's tiles; gst: 2·(G·S)·6 words of generator states (ping-pong);
 // fst: ocx_pipe_state_doubles(L); bad[nbatch]: set for a batch with a sequence the closed-form
 // comparator could not certify (its regret is NaN: the caller reruns that batch whole);
-// regret: nbatch·B doubles, batch k's at regret + k·B; fold(regret_k, B, fold_arg, stream)
-// after each batch (nullable).  The last batch may hold fewer runs (last_B <= B): it keeps the
+// regret: nbatch·B doubles, batch k's at regret + k·B; gmax (nullable): g(T) folded in by
+// each batch's last FTRL chunk.  The last batch may hold fewer runs (last_B <= B): it keeps the
 // layout's tiles, its spare sequences are padding.
 //
 // Registers decide where it pays.  The FTRL chunks run in the lean form (<= 128 VGPRs) beside
@@ -307,9 +305,8 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L) {
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,
-                                    double* regret, int64_t last_B,
-                                    hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
-                                    void* fold_arg, int nchunks, hipStream_t st) {
+                                    double* regret, int64_t last_B, unsigned long long* gmax,
+                                    int nchunks, hipStream_t st) {
     if (!ocx_trailing_supported(L) || nbatch <= 0 || !regret || !gst || !fst || !bad ||
         last_B < 1 || last_B > L->B)
         return hipErrorInvalidValue;
@@ -345,7 +342,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
         for (int64_t ci = 0; ci < nch; ++ci) {
             const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
             OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(lay(k), zt, yk, eta0, regret + k * L->B, 1, t0, tn,
-                                                   fst, bad + k, F));
+                                                   fst, bad + k, gmax, F));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)ci], F));
             if (!next) continue;
             // batch k+1's chunk ci, behind FTRL k's; its labels with the last chunk
@@ -356,7 +353,6 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
                                                 lastc ? nullptr : gst + (ci & 1) * words,
                                                 lastc ? 1 : 0, zt, yts[(k + 1) & 1], st));
         }
-        if (fold) OCX_PIPE_TRY(fold(regret + k * L->B, lay(k)->B, fold_arg, F));
     }
     OCX_PIPE_TRY(hipEventRecord(c.join_sim, F));
     OCX_PIPE_TRY(hipStreamWaitEvent(st, c.join_sim, 0));

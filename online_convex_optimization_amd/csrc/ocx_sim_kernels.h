@@ -22,9 +22,10 @@ hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const doub
 // the lean form over wave-groups [g0, g0 + gn) (<= 128 VGPRs; FTRL, 8 x 8 and 16 x 4 layouts),
 // the FTRL side of the overlapped pipeline (ocx_pipeline.hip)
 bool ocx_pipe_lean_supported(const ocx_layout* L);
+// gmax (nullable, device): g(T)'s bit pattern, max-folded in the kernel (ocx_max_fold's rule)
 hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const double* yt,
                                     double eta0, double* reg, int onepass, int64_t g0,
-                                    int64_t gn, hipStream_t st);
+                                    int64_t gn, unsigned long long* gmax, hipStream_t st);
 // FTRL over steps [t0, t0 + tn) of every sequence (t0 a multiple of 64), the step's state
 // carried in `state` (ocx_pipe_state_doubles(L) doubles) from the chunk before; the chunk that
 // ends at T writes the regrets (closed-form comparator only: onepass; a sequence it cannot
@@ -32,7 +33,8 @@ hipError_t ocx_launch_alg_pipe_lean(const ocx_layout* L, const double* zt, const
 int64_t ocx_pipe_state_doubles(const ocx_layout* L);
 hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, const double* yt,
                                      double eta0, double* reg, int onepass, int64_t t0,
-                                     int64_t tn, double* state, int* bad, hipStream_t st);
+                                     int64_t tn, double* state, int* bad,
+                                     unsigned long long* gmax, hipStream_t st);
 // g(T) sampler over sequences [b_off, b_off + nseq) of a d = 64 layout, at most wps waves per
 // SIMD (four-wave blocks; ocx_gen_wave.hip)
 // (wps >= 4: the 96-VGPR form, which spills a little; below: the 128-VGPR form)
@@ -40,7 +42,7 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
                                    int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
                                    hipStream_t st);
 // generation overlapped with FTRL (ocx_pipeline.hip): nbatch batches of L->B runs from run0,
-// regret = the last batch's, fold(regret_sub, n, fold_arg, stream) after every sub-batch
+// regret = the last batch's; gmax (nullable, device) max-folds g(T) over every batch
 bool ocx_pipeline_supported(const ocx_layout* L);
 bool ocx_pipeline_worth(const ocx_layout* L, int wps);
 // the multi-stream paths may fork from st (not under graph capture on HIP runtimes < 7.2)
@@ -53,9 +55,8 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
                               double* yt, hipStream_t st);
 hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                      int64_t nbatch, double* zt, double* yt, double eta0,
-                                     double* regret, int onepass,
-                                     hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
-                                     void* fold_arg, int wps, int64_t sub_seqs, hipStream_t st);
+                                     double* regret, int onepass, unsigned long long* gmax,
+                                     int wps, int64_t sub_seqs, hipStream_t st);
 // generation of batch k+1 trailing the chunked FTRL pass over batch k in one z buffer
 // (ocx_pipeline.hip: the capacity-limited batches); see there for the buffers
 bool ocx_trailing_supported(const ocx_layout* L);
@@ -64,9 +65,8 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L);
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,
-                                    double* regret, int64_t last_B,
-                                    hipError_t (*fold)(const double*, int64_t, void*, hipStream_t),
-                                    void* fold_arg, int nchunks, hipStream_t st);
+                                    double* regret, int64_t last_B, unsigned long long* gmax,
+                                    int nchunks, hipStream_t st);
 // rows [t_off, t_off + nrows) of L's full-horizon tile, streams fresh (st_in null) or resumed
 // from st_in, saved to st_out (nullable, not st_in); labels: then the T labels (ocx_gen_wave.hip)
 hipError_t ocx_launch_gen_gT_rows(const ocx_layout* L, uint64_t base_seed, int64_t run0,
