@@ -111,7 +111,7 @@ __device__ __forceinline__ double ocx_zj(const ocx_d2* zb, int j) {
 
 // Lane-local part of a tree total: the sequential sum of a lane's C products (with P = 1
 // the reference's order).  In-lane pairwise sums for P > 1 measured 1.5 % on the few-wave
-// T = 1e5 batch (profiles/r02_ab_lanesum.jsonl): not taken.
+// T = 1e5 batch (round 2; the record is in git history): not taken.
 template <int C>
 __device__ __forceinline__ double ocx_lane_sum(const double (&p)[C]) {
     double acc = 0.0;

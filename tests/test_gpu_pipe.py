@@ -39,7 +39,7 @@ def close_closed(a, b, T):
 
 # (lanes per sequence, d): C = d / P coordinates per lane in {4, 8, 16, 32}
 SHAPES = [(8, 32), (8, 64), (8, 128), (8, 256), (16, 64), (16, 128), (16, 512), (32, 128),
-          (32, 1024)]
+          (32, 1024), (64, 1024)]
 
 
 @pytest.mark.parametrize("P,d", SHAPES)
@@ -70,11 +70,11 @@ def test_pipe_kernel_matches_oracle(eng, P, d):
         assert close_closed(r1[:B], ref[0], T), (P, d, flag)
 
 
-@pytest.mark.parametrize("P", [8, 16, 32])
+@pytest.mark.parametrize("P", [8, 16, 32, 64])
 def test_pipe_kernel_exact_on_single_coordinate_rows(eng, P):
     """Flip / switching rows (one nonzero coordinate): exact ties q = y survive the
     pipelined step — regrets bit-identical to the reference's."""
-    d = 64 if P < 32 else 128
+    d = {8: 64, 16: 64, 32: 128, 64: 1024}[P]
     for fn in (O.flip_sequence, O.switching_two_leaders_sequence):
         z, y, _ = fn(1000, d=d)
         Z = np.repeat(z[None].astype(np.float64), 5, axis=0)
@@ -102,7 +102,8 @@ def test_pipe_kernel_long_horizon_drift(eng):
 
 
 @pytest.mark.parametrize("P,d,T,chunk", [(8, 64, 300, 64), (16, 64, 257, 128), (8, 128, 640, 192),
-                                         (32, 1024, 200, 64), (16, 512, 129, 64)])
+                                         (32, 1024, 200, 64), (16, 512, 129, 64),
+                                         (64, 1024, 300, 128)])
 def test_chunked_pipe_is_bit_identical(eng, P, d, T, chunk):
     """The pipelined kernel run in launches of `chunk` steps, its state carried through HBM
     (the trailing pipeline's FTRL side, ocx_test_alg_pipe_chunked), against one launch:

@@ -1,7 +1,7 @@
-"""End-to-end layout probe (round 3): generation + FTRL (closed-form comparator) of one
+"""End-to-end layout probe (round 3; rerun by tools/evidence.sh): generation + FTRL (closed-form comparator) of one
 resident d = 64 batch under several lane layouts.  One JSON line per layout: generator ms,
 FTRL ms, timesteps/s of the pair.
-    python tools/r03_e2e_layout.py [B] [T] [lanes,...]   (lanes 128 = OCX_LANES_BEST)"""
+    python tools/e2e_layout.py [B] [T] [lanes,...]   (lanes 128 = OCX_LANES_BEST)"""
 import json
 import math
 import os

@@ -19,13 +19,19 @@
 #   pipeab       FTRL/FTL kernel A/B over tuning builds (PIPEAB=main,pys,...: tools/pipe_lib_ab.py)
 #   alg          FTRL / FTL kernel times on the resident batches (tools/alg_probe.py)
 #   algsq        SQ counters of the pipelined FTRL / FTL kernels (tools/alg_sq.py, few-wave batch)
-#   overlap      tools/r04_overlap_probe.py (generation overlapped with FTRL vs sequential)
-#   pipe         tools/r04_pipe_probe.py (candidate-select FTRL/FTL step vs plain)
-#   overlap1e5   the same probe on the T = 1e5 batch (4 900 x 1e5 x 64), sub-batches below a round
+#   overlap      tools/overlap_probe.py (sub-batch overlap of generation and FTRL vs sequential)
 #   pipetraffic  FETCH_SIZE / WRITE_SIZE of the overlapped pipeline's kernels (tools/pipe_traffic.py)
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
+#   trail        tools/trail_probe.py (trailing pipeline vs sequential: configs[4], configs[3] T=1e5)
+#   trailtrace   rocprofv3 --kernel-trace of the trailing pipeline on the T = 1e5 case
+#   genscale     tools/genscale_probe.py (d = 1024 generator time vs streams per SIMD)
+#   cumask       tools/cumask_map (CU-mask placement) and tools/cumask_probe.py (CU-split overlap)
 #   config3      tools/perf_extra.py config3 (configs[2]: FTRL vs exact FTL, generation included)
 #   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
+#   layout       tools/e2e_layout.py (generation + FTRL by lane layout, d = 64)
+#   smalld       tools/gt_small_d.py (g(T) layouts for 4 <= d < 64)
+#   smart        tools/smart_probe.py (SMART kernels)
+#   exact        tools/exact_probe.py (the general exact comparator)
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
@@ -82,27 +88,45 @@ for step in "$@"; do
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d "${O}_algsq" -o sq -- python3 "$R/tools/alg_sq.py" ${ALGSQ_SHAPE:-4900 100000 64} > "${O}_algsq.log" 2>&1) || fail algsq $?
     python tools/pmc_summary.py --kernel alg_pipe "${O}_algsq" ;;
   overlap)
-    timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?
+    timeout -k 10 400 python -u tools/overlap_probe.py > "${O}_overlap.jsonl" 2> "${O}_overlap.err" || fail overlap $?
     cut -c1-260 "${O}_overlap.jsonl" ;;
-  pipe)
-    timeout -k 10 400 python -u tools/r04_pipe_probe.py > "${O}_pipe.jsonl" 2> "${O}_pipe.err" || fail pipe $?
-    cut -c1-200 "${O}_pipe.jsonl" ;;
-  overlap1e5)
-    # the capacity-limited T = 1e5 batch (4 900 x 1e5 x 64): sub-batches smaller than a round
-    OCX_PROBE_B=4900 OCX_PROBE_T=100000 OCX_PROBE_NB=2 OCX_PROBE_CONFIGS=${O1E5_CONFIGS:-4:0:2456:128:2:2,4:0:1232:128:2:2,4:0:0:128:2:2} timeout -k 10 400 python -u tools/r04_overlap_probe.py > "${O}_overlap1e5.jsonl" 2> "${O}_overlap1e5.err" || fail overlap1e5 $?
-    cut -c1-300 "${O}_overlap1e5.jsonl" ;;
   pipetraffic)
     # HBM bytes of the overlapped pipeline's kernels (two PMC passes over two batches; the
     # counters serialise the dispatches, so these runs are for bytes, not time)
     for C in FETCH_SIZE WRITE_SIZE; do
-      (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_SEQ=0 OCX_PROBE_CONFIGS=4:0:0:128:2:2 timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "${O}_ppmc_$C" -o pmc -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_ppmc_$C.log" 2>&1) || fail "pipe pmc $C" $?
+      (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=2 OCX_PROBE_SEQ=0 OCX_PROBE_CONFIGS=4:0:2:2 timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "${O}_ppmc_$C" -o pmc -- python3 "$R/tools/overlap_probe.py" > "${O}_ppmc_$C.log" 2>&1) || fail "pipe pmc $C" $?
     done
     python tools/pipe_traffic.py "${O}_ppmc_FETCH_SIZE" "${O}_ppmc_WRITE_SIZE" > "${O}_pipetraffic.json" || fail pipetraffic $?
     cat "${O}_pipetraffic.json" ;;
   overlaptrace)
-    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_SIDES=0 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:0:128:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/r04_overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
+    (cd /tmp && export TMPDIR=/tmp && OCX_PROBE_NB=4 OCX_PROBE_CONFIGS=${OTRACE_CONFIG:-4:0:2:2} timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_otrace" -o ot --output-format csv -- python3 "$R/tools/overlap_probe.py" > "${O}_otrace.log" 2>&1) || fail overlaptrace $?
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
     cut -c1-400 "${O}_otrace.json" ;;
+  trail)
+    timeout -k 10 600 python -u tools/trail_probe.py --cases "${TRAIL_CASES:-c4,t1e5}" --chunks "${TRAIL_CHUNKS:-12}" > "${O}_trail.jsonl" 2> "${O}_trail.err" || fail trail $?
+    cut -c1-260 "${O}_trail.jsonl" ;;
+  trailtrace)
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_ttrace" -o tt --output-format csv -- python3 "$R/tools/trail_probe.py" --cases t1e5 --runs-t5 19600 --check 0 > "${O}_ttrace.log" 2>&1) || fail trailtrace $?
+    ls "${O}_ttrace" ;;
+  genscale)
+    timeout -k 10 300 python -u tools/genscale_probe.py > "${O}_genscale.jsonl" 2> "${O}_genscale.err" || fail genscale $?
+    cat "${O}_genscale.jsonl" ;;
+  cumask)
+    timeout -k 10 60 tools/cumask_map > "${O}_cumask_map.txt" 2>&1 || fail cumask_map $?
+    timeout -k 10 240 python -u tools/cumask_probe.py > "${O}_cumask.jsonl" 2> "${O}_cumask.err" || fail cumask $?
+    cat "${O}_cumask_map.txt" "${O}_cumask.jsonl" ;;
+  layout)
+    timeout -k 10 400 python -u tools/e2e_layout.py > "${O}_layout.jsonl" 2> "${O}_layout.err" || fail layout $?
+    cut -c1-200 "${O}_layout.jsonl" ;;
+  smalld)
+    timeout -k 10 400 python -u tools/gt_small_d.py > "${O}_smalld.jsonl" 2> "${O}_smalld.err" || fail smalld $?
+    cut -c1-200 "${O}_smalld.jsonl" ;;
+  smart)
+    timeout -k 10 400 python -u tools/smart_probe.py > "${O}_smart.jsonl" 2> "${O}_smart.err" || fail smart $?
+    cut -c1-200 "${O}_smart.jsonl" ;;
+  exact)
+    timeout -k 10 400 python -u tools/exact_probe.py > "${O}_exact.jsonl" 2> "${O}_exact.err" || fail exact $?
+    cut -c1-200 "${O}_exact.jsonl" ;;
   config3)
     # configs[2]: FTRL vs exact FTL, 1e5 trials x 1e4 x 64, generation included
     timeout -k 10 600 python tools/perf_extra.py config3 > "${O}_config3.log" 2>&1 || fail config3 $?

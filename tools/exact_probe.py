@@ -1,4 +1,4 @@
-"""General exact-FTL solver timing probe (round 3): ocx_dev_exact_ball_solve_tiled on the
+"""General exact-FTL solver timing probe (round 3; rerun by tools/evidence.sh): ocx_dev_exact_ball_solve_tiled on the
 exact driver's shapes (d = 5, every prefix of T = 100..1000, the linf ball, on the i.i.d.
 family's clipped rows), and the exact g(T) comparator (final prefix only, 200 runs).  One
 JSON line per shape: kernel ms, problems/s, mean Newton steps, max certified gap."""

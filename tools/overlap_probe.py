@@ -1,10 +1,12 @@
-"""Round 4: generation overlapped with FTRL (ocx_dev_gen_simulate, csrc/ocx_pipeline.hip)
+"""Generation overlapped with FTRL in sub-batches (ocx_dev_gen_simulate, csrc/ocx_pipeline.hip)
 against the sequential gen-then-FTRL loop, on the bench's resident batch (32 768 x 1e4 x 64,
 OCX_LANES_BEST).  One JSON line per configuration: ms per batch, timesteps/s, fraction of
 2*(8d+8) B/step, and whether the regrets and g(T) are bit-identical to the sequential path.
-Knobs per line: OCX_PIPE_WPS (generator waves per SIMD), OCX_PIPE_CAND (FTRL step form),
-sub_seqs (sequences per sub-batch; 0 = one generator round), OCX_PIPE_GEN_STREAMS /
-OCX_PIPE_SIM_STREAMS (sub-batches alternating over one or two streams per side)."""
+Knobs per configuration (OCX_PROBE_CONFIGS="wps:sub:gs:ss,..."): OCX_PIPE_WPS (generator waves
+per SIMD), sub_seqs (sequences per sub-batch; 0 = one generator round), OCX_PIPE_GEN_STREAMS /
+OCX_PIPE_SIM_STREAMS (sub-batches alternating over one or two streams per side).
+OCX_PROBE_SIDES=1 also times each side alone through OCX_PIPE_SKIP, which only a tuning build
+compiled with -DOCX_PIPE_TUNE_SKIP honours (OCX_LIB)."""
 import json
 import math
 import os
@@ -30,23 +32,18 @@ def run(db, nb, pipelined, sub=0):
 
 
 def _configs():
-    # (generator waves per SIMD, candidate-select FTRL step, sub-batch sequences, FTRL VGPRs,
-    # generator streams, FTRL streams)
-    configs = [("4", "0", 0, "128", "2", "2"), ("4", "0", 0, "128", "1", "1"),
-               ("3", "0", 0, "128", "2", "2"), ("3", "0", 0, "168", "2", "2"),
-               ("4", "0", 2 * 1024, "128", "2", "2")]
+    # (generator waves per SIMD, sub-batch sequences, generator streams, FTRL streams)
+    configs = [("4", 0, "2", "2"), ("4", 0, "1", "1"), ("3", 0, "2", "2"), ("4", 2 * 1024, "2", "2")]
     if os.environ.get("OCX_PROBE_CONFIGS"):
         configs = []
         for c in os.environ["OCX_PROBE_CONFIGS"].split(","):
-            f = c.split(":") + ["1", "1"]
-            configs.append((f[0], f[1], int(f[2]), f[3], f[4], f[5]))
+            f = c.split(":") + ["2", "2"]
+            configs.append((f[0], int(f[1]), f[2], f[3]))
     return configs
 
 
-def _env(wps, cand, lean, gs, ss):
+def _env(wps, gs, ss):
     os.environ["OCX_PIPE_WPS"] = wps
-    os.environ["OCX_PIPE_CAND"] = cand
-    os.environ["OCX_PIPE_LEAN"] = lean
     os.environ["OCX_PIPE_GEN_STREAMS"] = gs
     os.environ["OCX_PIPE_SIM_STREAMS"] = ss
 
@@ -62,8 +59,8 @@ def main():
     seq = os.environ.get("OCX_PROBE_SEQ", "1") != "0"
     configs = _configs()
     if not seq:
-        for wps, cand, sub, lean, gs, ss in configs:
-            _env(wps, cand, lean, gs, ss)
+        for wps, sub, gs, ss in configs:
+            _env(wps, gs, ss)
             ms, r, g = run(db, nb, True, sub)
             print(json.dumps({"B": B, "T": T, "mode": "pipelined", "ms_per_batch": ms}), flush=True)
         return
@@ -80,19 +77,18 @@ def main():
     print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "sequential",
                       "ms_per_batch": ms0, "timesteps_per_s": rate(ms0),
                       "frac_1040": rate(ms0) * 1040 / 8e12, "gmax": g0, **parts}), flush=True)
-    for wps, cand, sub, lean, gs, ss in configs:
-        _env(wps, cand, lean, gs, ss)
-        # each side alone (tuning knob OCX_PIPE_SKIP: outputs wrong, times only)
+    for wps, sub, gs, ss in configs:
+        _env(wps, gs, ss)
+        # each side alone (OCX_PIPE_SKIP, tuning builds only: outputs wrong, times only)
         side = {}
-        # OCX_PROBE_SIDES=0 (the kernel-trace step): the pipelined run alone
-        for skip in (("sim", "gen") if os.environ.get("OCX_PROBE_SIDES", "1") != "0" else ()):
+        for skip in (("sim", "gen") if os.environ.get("OCX_PROBE_SIDES", "0") == "1" else ()):
             os.environ["OCX_PIPE_SKIP"] = skip
             side["gen_only_ms" if skip == "sim" else "sim_only_ms"] = run(db, nb, True, sub)[0]
         os.environ.pop("OCX_PIPE_SKIP", None)
         ms, r, g = run(db, nb, True, sub)
         print(json.dumps({"B": B, "T": T, "layout": [db.L.P, db.L.C], "mode": "pipelined",
-                          "wps": int(wps), "cand": cand == "1", "sub_seqs": sub,
-                          "ftrl_vgprs": int(lean), "gen_streams": int(gs), "sim_streams": int(ss),
+                          "wps": int(wps), "sub_seqs": sub,
+                          "gen_streams": int(gs), "sim_streams": int(ss),
                           "ms_per_batch": ms, "timesteps_per_s": rate(ms),
                           "frac_1040": rate(ms) * 1040 / 8e12, "gmax": g, **side,
                           "bitidentical": bool(np.array_equal(r, r0)) and g == g0}), flush=True)

@@ -1,4 +1,4 @@
-"""SMART timing probe (round 3): the O(T²·d) re-scan kernels vs the O(T·d) closed-prefix
+"""SMART timing probe (round 3; rerun by tools/evidence.sh): the O(T²·d) re-scan kernels vs the O(T·d) closed-prefix
 kernel on g(T)-sampler batches, next to the FTL kernel on the same batch.  One JSON line per
 configuration."""
 import json
