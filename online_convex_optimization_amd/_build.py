@@ -75,23 +75,28 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
     return LIB
 
 
-def build_variant(name: str, defines, jobs: int = 4, source: str = "ocx_sim.hip",
+def build_variant(name: str, defines, jobs: int = 4, source="ocx_sim.hip",
                   out_dir: str = None) -> str:
-    """Tuning variant: one source recompiled with -D overrides, linked with the other
-    objects into <out_dir, default tune_build>/libocx_<name>.so (never loaded by the product
-    path; select it with OCX_LIB)."""
+    """Tuning variant: one source (or a list of sources) recompiled with -D overrides, linked
+    with the other objects into <out_dir, default tune_build>/libocx_<name>.so (never loaded by
+    the product path; select it with OCX_LIB)."""
     hipcc = _hipcc()
     out_dir = out_dir or os.path.join(ROOT, "tune_build")
     os.makedirs(out_dir, exist_ok=True)
     build(jobs=jobs)  # the shared objects of the other sources
-    obj = os.path.join(out_dir, f"{source.replace('.hip', '')}_{name}.o")
+    srcs = [source] if isinstance(source, str) else list(source)
     lib = os.path.join(out_dir, f"libocx_{name}.so")
     dflags = [f"-D{d}" for d in defines]
-    src = os.path.join(CSRC, source)
-    if _stale(lib, [src, *[os.path.join(CSRC, h) for h in HEADERS]]):
-        subprocess.run([hipcc, *CFLAGS, *dflags, "-c", src, "-o", obj], check=True)
-        others = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES if s != source]
-        subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", obj, *others, "-o", lib],
+    deps = [os.path.join(CSRC, s) for s in srcs] + [os.path.join(CSRC, h) for h in HEADERS]
+    if _stale(lib, deps):
+        objs = []
+        for sname in srcs:
+            obj = os.path.join(out_dir, f"{sname.replace('.hip', '')}_{name}.o")
+            subprocess.run([hipcc, *CFLAGS, *dflags, "-c", os.path.join(CSRC, sname), "-o", obj],
+                           check=True)
+            objs.append(obj)
+        others = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES if s not in srcs]
+        subprocess.run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, *others, "-o", lib],
                        check=True)
     return lib
 

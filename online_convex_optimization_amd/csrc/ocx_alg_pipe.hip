@@ -483,8 +483,11 @@ bool ocx_pipe_lean_supported(const ocx_layout* L) {
 namespace {
 // the d = 1024 lean block's LDS request: a CU's 160 KiB less two generator blocks (4 x 1 088
 // doubles each, ocx_gen_wave.hip ring_doubles) and a margin, so one FTRL block and two generator
-// blocks share a CU
-constexpr size_t kLeanLds1k = 160 * 1024 - 2 * 4 * 1088 * 8 - 4096;
+// blocks share a CU (OCX_TRAIL_1K_GEN_BESIDE, tuning: generator blocks per CU beside it)
+#ifndef OCX_TRAIL_1K_GEN_BESIDE
+#define OCX_TRAIL_1K_GEN_BESIDE 2
+#endif
+constexpr size_t kLeanLds1k = 160 * 1024 - OCX_TRAIL_1K_GEN_BESIDE * 4 * 1088 * 8 - 4096;
 
 hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
     const dim3 grid = ocx_grid(a.gn, 1), block(64);

@@ -294,7 +294,10 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L) {
     const int64_t simds = 4 * (int64_t)cus, S = L->S;
     // generator waves that fit on a SIMD beside an FTRL wave / on one without
     const bool k1 = L->d == 1024;
-    const int64_t beside = k1 ? 2 : 4, alone = k1 ? 4 : 6;
+#ifndef OCX_TRAIL_1K_GEN_BESIDE
+#define OCX_TRAIL_1K_GEN_BESIDE 2
+#endif
+    const int64_t beside = k1 ? OCX_TRAIL_1K_GEN_BESIDE : 4, alone = k1 ? 4 : 6;
     int64_t b = simds * alone;
     while (b > S) {
         const int64_t nf = std::min(simds, (b + S - 1) / S);
