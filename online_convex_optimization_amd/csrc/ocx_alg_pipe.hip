@@ -36,7 +36,6 @@
 // the second comparator pass: a sequence the closed form cannot certify gets a NaN regret
 // and raises *bad (the caller runs its batch again in the sequential path).
 #include <cmath>
-#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -90,23 +89,22 @@ struct PipeArgs {
     double* state;   // chunked runs: the carried state (nullable: whole run)
     int* bad;        // chunked runs: set when a sequence needs the second pass
     unsigned long long* gmax;  // nullable: g(T) = max(0, max regret) folded in (bit pattern)
-    int64_t nw;      // grid-stride kernels (GS): waves launched; wave w runs groups w, w + nw, ..
 };
 
 // RT (FTRL): the rescale's sqrt only in waves where a sequence may need the rescale (see the
 // step).  CHUNK: a chunked run (t0, tn, state); the whole-run kernels compile without it, so
 // its bookkeeping costs them no registers (the lean form spilled with it: 148 B per lane).
 template <int C, int P, int NB, bool FTL, bool RT, bool CHUNK = false>
-__device__ __forceinline__ void alg_pipe_body(const PipeArgs& a, const int64_t wv) {
+__device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
     static_assert(P >= 2 && NB >= 4, "butterfly layouts, a ring holding z_{t-1} .. z_{t+1}");
     using IT = typename std::conditional<(C <= OCX_PIPE_IT32_MAXC), int, int64_t>::type;
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     constexpr int NS = pipe_state_words(C);
     const int lane = threadIdx.x & 63;
-    // wv: wave-uniform, provably (readfirstlane in the kernel): the tile bases live in SGPRs
-    // and every load is an SGPR base + the lane's constant offset, with no per-load address
-    // arithmetic
+    // wave-uniform, provably (readfirstlane): the tile bases live in SGPRs and every load
+    // is an SGPR base + the lane's constant offset, with no per-load address arithmetic
+    const int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_pipe_wave_id(a.gn));
     if (wv >= a.gn) return;
     const int64_t g = a.g0 + wv;
     const int64_t T = a.T, t0 = CHUNK ? a.t0 : 0, tn = CHUNK ? a.tn : T;
@@ -342,18 +340,9 @@ template <int C, int P, int MINW>
 constexpr bool pipe_rt() {
     return !(C == 8 && P == 8 && MINW == 1);
 }
-// GS (grid-stride): a fixed grid of a.nw waves, wave w running groups w, w + nw, .. one after
-// the other — the d = 1024 lean form, whose launch must hold one wave per SIMD (below).
-template <int C, int P, int NB, bool FTL, int MINW = 1, bool CHUNK = false, bool GS = false>
+template <int C, int P, int NB, bool FTL, int MINW = 1, bool CHUNK = false>
 __global__ __launch_bounds__(OCX_BLOCK, MINW) void ocx_alg_pipe_kernel(PipeArgs a) {
-    if constexpr (GS) {
-        const int64_t w0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-        for (int64_t wv = (int64_t)__builtin_amdgcn_readfirstlane((int)w0); wv < a.gn; wv += a.nw)
-            alg_pipe_body<C, P, NB, FTL, pipe_rt<C, P, MINW>(), CHUNK>(a, wv);
-    } else {
-        alg_pipe_body<C, P, NB, FTL, pipe_rt<C, P, MINW>(), CHUNK>(
-            a, (int64_t)__builtin_amdgcn_readfirstlane((int)ocx_pipe_wave_id(a.gn)));
-    }
+    alg_pipe_body<C, P, NB, FTL, pipe_rt<C, P, MINW>(), CHUNK>(a);
 }
 
 namespace {
@@ -436,7 +425,9 @@ PipeArgs pipe_args(const ocx_layout* L, const double* zt, const double* yt, doub
 
 // The pipelined step pays where one wave's step latency sets the batch time: the few-wave
 // butterfly layouts OCX_LANES_BEST chooses (8 x 8, 16 x 4 at d = 64; 16 x 16; 32 x 32 at
-// d = 1024) and their neighbours.  Other butterfly layouts keep the plain kernel.
+// d = 1024) and their neighbours, and 64 x 16 at d = 1024 (lanes_per_seq = 64: 17.3 vs 19.2 ms
+// for the 32 x 32 layout's pass over 2 688 x 5 000 steps, profiles/r05_genscale.jsonl).  Other
+// butterfly layouts keep the plain kernel.
 bool ocx_pipe_supported(const ocx_layout* L) {
     // T < 2^30: the step counter is a 32-bit int (ocx_ring_loop<..., int>)
     return !L->chain && L->T < ((int64_t)1 << 30) &&
@@ -462,13 +453,6 @@ int64_t ocx_pipe_state_doubles(const ocx_layout* L) {
 // (OCX_PIPE_LEAN_NB8 / _NB4 slots at 8 / 4 coordinates per lane) is what makes it fit.  FTRL
 // only, the pipelines' algorithm; 8 x 8 and 16 x 4 layouts.  One-wave blocks: the dispatcher
 // spreads them over the SIMDs the generator leaves room on.
-//
-// d = 1024 (the trailing pipeline only): its generator waves take 128 VGPRs, and no layout of
-// 1 024 coordinates fits a 128-VGPR FTRL wave (16 coordinates per lane, the fewest a wave can
-// hold, need a 4-slot ring of 128 VGPRs alone).  So the pairing there is two generator waves
-// and one FTRL wave of <= 256 VGPRs per SIMD: the 64 x 16 layout (one sequence per wave), a
-// grid of one four-wave block per CU whose LDS request (kLeanLds1k) leaves room for exactly two
-// generator blocks, each wave running its share of the batch's sequences one after the other.
 #ifndef OCX_PIPE_LEAN_NB8
 #define OCX_PIPE_LEAN_NB8 4
 #endif
@@ -476,19 +460,10 @@ int64_t ocx_pipe_state_doubles(const ocx_layout* L) {
 #define OCX_PIPE_LEAN_NB4 8
 #endif
 bool ocx_pipe_lean_supported(const ocx_layout* L) {
-    return !L->chain && L->T < ((int64_t)1 << 30) &&
-           ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4) || (L->P == 64 && L->C == 16));
+    return !L->chain && L->T < ((int64_t)1 << 30) && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
 }
 
 namespace {
-// the d = 1024 lean block's LDS request: a CU's 160 KiB less two generator blocks (4 x 1 088
-// doubles each, ocx_gen_wave.hip ring_doubles) and a margin, so one FTRL block and two generator
-// blocks share a CU (OCX_TRAIL_1K_GEN_BESIDE, tuning: generator blocks per CU beside it)
-#ifndef OCX_TRAIL_1K_GEN_BESIDE
-#define OCX_TRAIL_1K_GEN_BESIDE 2
-#endif
-constexpr size_t kLeanLds1k = 160 * 1024 - OCX_TRAIL_1K_GEN_BESIDE * 4 * 1088 * 8 - 4096;
-
 hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
     const dim3 grid = ocx_grid(a.gn, 1), block(64);
     if (L->P == 8 && L->C == 8) {
@@ -501,20 +476,6 @@ hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
             hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4, true>), grid, block, 0, st, a);
         else
             hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 16, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
-    } else if (L->P == 64 && L->C == 16) {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            cus = 256;
-        PipeArgs g = a;
-        const int64_t nblk = std::max<int64_t>(1, std::min<int64_t>(cus, (a.gn + 3) / 4));
-        g.nw = nblk * 4;
-        if (a.state)
-            hipLaunchKernelGGL((ocx_alg_pipe_kernel<16, 64, 4, false, 2, true, true>), dim3((unsigned)nblk),
-                               dim3(256), kLeanLds1k, st, g);
-        else
-            hipLaunchKernelGGL((ocx_alg_pipe_kernel<16, 64, 4, false, 2, false, true>), dim3((unsigned)nblk),
-                               dim3(256), kLeanLds1k, st, g);
     } else {
         return hipErrorInvalidValue;
     }
@@ -542,8 +503,7 @@ hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, cons
                                      unsigned long long* gmax, hipStream_t st) {
     if (L->G == 0 || tn <= 0) return hipSuccess;
     // onepass only: a chunk after the first cannot stream the second comparator pass
-    if (t0 < 0 || t0 % 64 != 0 || t0 + tn > L->T || !state || !onepass ||
-        !(ocx_pipe_supported(L) || ocx_pipe_lean_supported(L)))
+    if (t0 < 0 || t0 % 64 != 0 || t0 + tn > L->T || !state || !onepass || !ocx_pipe_supported(L))
         return hipErrorInvalidValue;
     PipeArgs a = pipe_args(L, zt, yt, eta0, reg, nullptr, nullptr, nullptr, onepass);
     a.t0 = t0;

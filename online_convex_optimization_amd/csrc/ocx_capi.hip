@@ -1006,20 +1006,15 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         // chunked FTRL pass over batch k, in the same z buffer (OCX_TRAILING=0: the sequential
         // loop below).  Its second label tile comes out of the budget.
         const char* te = std::getenv("OCX_TRAILING");
-        // its layout: the batch's own, except at d = 1024, where the FTRL side needs the 64 x 16
-        // layout (ocx_alg_pipe.hip: the only d = 1024 form that fits beside generator waves)
-        const int tlanes = (lanes_per_seq == OCX_LANES_BEST && d == 1024) ? 64 : lanes_per_seq;
-        ocx_layout Lt;
-        if (int rc = ocx_layout_init(chunk, T, d, tlanes, &Lt)) return rc;
         bool trail = !pipe && onepass && (!te || std::atoi(te) != 0) &&
-                     ocx_trailing_supported(&Lt) && R > chunk;
+                     ocx_trailing_supported(&Lp) && R > chunk;
         if (trail) {
-            const int64_t per_trail = per_seq + 8 * T + 64 * 8 * (2 * (int64_t)Lt.C + 7);
+            const int64_t per_trail = per_seq + 8 * T + 64 * 8 * (2 * (int64_t)Lp.C + 7);
             int64_t c2 = std::max<int64_t>(64, std::min<int64_t>(budget / per_trail, R));
             const int64_t nb2 = (R + c2 - 1) / c2;
             c2 = (R + nb2 - 1) / nb2;
             // and no more streams than fit beside the FTRL waves in one generator round
-            const int64_t cap = ocx_trailing_max_batch(&Lt);
+            const int64_t cap = ocx_trailing_max_batch(&Lp);
             if (c2 > cap) {
                 const int64_t nb3 = (R + cap - 1) / cap;
                 c2 = (R + nb3 - 1) / nb3;
@@ -1027,19 +1022,18 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             if (c2 < chunk) {
                 chunk = c2;
                 if (int rc = ocx_layout_init(chunk, T, d, lanes_per_seq, &Lp)) return rc;
-                if (int rc = ocx_layout_init(chunk, T, d, tlanes, &Lt)) return rc;
                 OCX_HIP(cx->out.ensure((size_t)chunk * 8));
             }
-            trail = ocx_trailing_supported(&Lt) && R > chunk;
+            trail = ocx_trailing_supported(&Lp) && R > chunk;
         }
         if (trail) {
             // every batch, the last one holding the remainder in the same tiles
             const int64_t nfull = (R + chunk - 1) / chunk, last_B = R - (nfull - 1) * chunk;
-            OCX_HIP(cx->zt.ensure((size_t)Lt.z_elems * 8));
-            OCX_HIP(cx->yt.ensure((size_t)Lt.y_elems * 8));
-            OCX_HIP(cx->yt2.ensure((size_t)Lt.y_elems * 8));
-            OCX_HIP(cx->gst.ensure((size_t)2 * Lt.G * Lt.S * 6 * 8));
-            OCX_HIP(cx->fst.ensure((size_t)ocx_pipe_state_doubles(&Lt) * 8));
+            OCX_HIP(cx->zt.ensure((size_t)Lp.z_elems * 8));
+            OCX_HIP(cx->yt.ensure((size_t)Lp.y_elems * 8));
+            OCX_HIP(cx->yt2.ensure((size_t)Lp.y_elems * 8));
+            OCX_HIP(cx->gst.ensure((size_t)2 * Lp.G * Lp.S * 6 * 8));
+            OCX_HIP(cx->fst.ensure((size_t)ocx_pipe_state_doubles(&Lp) * 8));
             OCX_HIP(cx->bad.ensure((size_t)nfull * sizeof(int)));
             double* rdst = regrets_on_device ? regrets : nullptr;
             if (!rdst) {
@@ -1052,7 +1046,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             // run ahead) measured no better (profiles/r05_trail_pace.jsonl, r05_trail_chunks.jsonl)
             int nch = 12;
             if (const char* e = std::getenv("OCX_TRAIL_CHUNKS")) nch = std::max(2, std::atoi(e));
-            OCX_HIP(ocx_run_gen_sim_trailing(&Lt, base_seed, run0, nfull, cx->zt.as<double>(),
+            OCX_HIP(ocx_run_gen_sim_trailing(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
                                              cx->yt.as<double>(), cx->yt2.as<double>(),
                                              cx->gst.as<uint64_t>(), cx->fst.as<double>(),
                                              cx->bad.as<int>(), eta0, rdst, last_B,
@@ -1067,7 +1061,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
                 for (int64_t k = 0; k < nfull; k += test_unclean_every) hb[(size_t)k] = 1;
             for (int64_t k = 0; k < nfull; ++k) {
                 if (!hb[(size_t)k]) continue;
-                ocx_layout Lk = Lt;  // the last batch: same tiles, last_B runs
+                ocx_layout Lk = Lp;  // the last batch: same tiles, last_B runs
                 if (k + 1 == nfull) Lk.B = last_B;
                 OCX_HIP(ocx_launch_gen_gT(&Lk, base_seed, run0 + k * chunk, cx->zt.as<double>(),
                                           cx->yt.as<double>(), st));

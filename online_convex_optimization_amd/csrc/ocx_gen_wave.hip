@@ -869,13 +869,8 @@ __host__ __device__ constexpr int gen_block(int DF, bool LR, int OV = 0) {
 // Waves per SIMD the register allocation must allow.  The d = 64 kernels' rings (4.6 KB per
 // wave) and tables (6 KB per block) admit six waves per SIMD in LDS; the default form keeps
 // the four-wave register budget (no spills), the few-stream form (LR) asks for six.
-// OCX_GENW_MIN_WAVES_1K: the d = 1024 form's budget (tuning: 6 gives 80 VGPRs, which would let
-// three generator waves share a SIMD with a 256-VGPR FTRL wave, at 61 spilled VGPRs)
-#ifndef OCX_GENW_MIN_WAVES_1K
-#define OCX_GENW_MIN_WAVES_1K 4
-#endif
 #ifndef OCX_GENW_MIN_WAVES
-#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? OCX_GENW_MIN_WAVES_1K : 1))
+#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? 4 : 1))
 #else
 #define OCX_GENW_MIN_WAVES_FOR(DF, LR) OCX_GENW_MIN_WAVES
 #endif

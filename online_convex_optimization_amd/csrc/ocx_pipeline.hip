@@ -274,14 +274,16 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 // each batch's last FTRL chunk.  The last batch may hold fewer runs (last_B <= B): it keeps the
 // layout's tiles, its spare sequences are padding.
 //
-// Registers decide where it pays.  At d = 64 the FTRL chunks run in the lean form (<= 128
-// VGPRs) beside generator waves of the few-stream form (80 VGPRs: six per SIMD alone, four
-// beside an FTRL wave).  d = 1024's generator waves take 128 VGPRs and no 128-VGPR FTRL form of
-// 1 024 coordinates exists, so there one FTRL wave of the 64 x 16 layout (<= 256 VGPRs, one
-// block per CU) shares each SIMD with two generator waves — and two generator waves per SIMD
-// already run at the rate of three (2 048 vs 2 688 streams x 5 000 x 1 024: 38.0 vs 48.4 ms,
-// profiles/r05_genscale.jsonl).  A batch is capped where every generator wave still fits beside
-// the FTRL waves (ocx_trailing_max_batch: 8 x 8 at d = 64 ≈4 900 streams; d = 1024: 2 048).
+// Registers decide where it pays.  The FTRL chunks run in the lean form (<= 128 VGPRs) beside
+// generator waves of the few-stream form (80 VGPRs: six per SIMD alone, four beside an FTRL
+// wave), so a batch is capped where every generator wave still fits beside the FTRL waves
+// (ocx_trailing_max_batch; 8 x 8 at d = 64: ≈4 900 streams).  d = 1024 keeps the sequential
+// loop: its generator waves take 128 VGPRs and no 1 024-coordinate FTRL wave fits in 128, and
+// the pairings that do fit measured slower than sequential (2.22e8 timesteps/s): the 32 x 32
+// full form 2.15e8; a 64 x 16 grid-stride form (one FTRL wave of 256 VGPRs beside two generator
+// waves per SIMD) 1.98e8, and beside three 80-VGPR generator waves 2.17e8 — the generator's
+// chunks ran 9–13 ms beside the FTRL chunks against 7.3 ms alone (profiles/r05_trail_c4*.jsonl,
+// DESIGN.md §3.8).
 bool ocx_trailing_supported(const ocx_layout* L) {
     return ocx_pipe_lean_supported(L) && L->T >= 128 && L->T * L->d < ((int64_t)1 << 32);
 }
@@ -292,16 +294,11 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const int64_t simds = 4 * (int64_t)cus, S = L->S;
-    // generator waves that fit on a SIMD beside an FTRL wave / on one without
-    const bool k1 = L->d == 1024;
-#ifndef OCX_TRAIL_1K_GEN_BESIDE
-#define OCX_TRAIL_1K_GEN_BESIDE 2
-#endif
-    const int64_t beside = k1 ? OCX_TRAIL_1K_GEN_BESIDE : 4, alone = k1 ? 4 : 6;
-    int64_t b = simds * alone;
+    // generator waves that fit: 4 on a SIMD beside an FTRL wave, 6 on one without
+    int64_t b = simds * 6;
     while (b > S) {
         const int64_t nf = std::min(simds, (b + S - 1) / S);
-        if (nf * beside + (simds - nf) * alone >= b) break;
+        if (nf * 4 + (simds - nf) * 6 >= b) break;
         b -= S;
     }
     return b;

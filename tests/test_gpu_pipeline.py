@@ -146,26 +146,22 @@ def _capacity_limited(monkeypatch, gb):
     monkeypatch.setenv("OCX_MIN_RESIDENT", "16")
 
 
-@pytest.mark.parametrize("T,d,runs,gb,chunks,lanes", [(2000, 64, 1000, 0.35, "8", 128),
-                                                      (700, 64, 900, 0.06, "3", 128),
-                                                      (640, 1024, 130, 0.25, "4", 64),
-                                                      (320, 1024, 70, 0.05, "2", 64),
-                                                      (300, 64, 500, 0.02, "2", 128)])
-def test_trailing_equals_sequential(eng, monkeypatch, T, d, runs, gb, chunks, lanes):
+@pytest.mark.parametrize("T,d,runs,gb,chunks", [(2000, 64, 1000, 0.35, "8"), (700, 64, 900, 0.06, "3"),
+                                                (640, 1024, 130, 0.25, "4"), (300, 64, 500, 0.02, "2")])
+def test_trailing_equals_sequential(eng, monkeypatch, T, d, runs, gb, chunks):
     """Regrets (host and device-resident) and g(T) of the trailing path equal the sequential
     loop's bit for bit, over several batches and a smaller last one, and sampled sequences are
-    within the closed-form bar of the oracle.  d = 1024 trails in the 64 x 16 layout (one
-    sequence per FTRL wave, ocx_alg_pipe.hip's grid-stride lean form), so the sequential loop
-    is asked for the same layout (lanes 64)."""
+    within the closed-form bar of the oracle."""
     import torch
     _capacity_limited(monkeypatch, gb)
     monkeypatch.setenv("OCX_TRAIL_CHUNKS", chunks)
     out = {}
     for trail in ("0", "1"):
         monkeypatch.setenv("OCX_TRAILING", trail)
-        reg = eng.gT_regrets(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=lanes)
-        gm = eng.gT_max(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=lanes)
-        dev = eng.gT_regrets_device(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=lanes)
+        reg = eng.gT_regrets(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
+        gm = eng.gT_max(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
+        dev = eng.gT_regrets_device(T, runs, base_seed=3, d=d, run0=11,
+                                    lanes_per_seq=eng.LANES_BEST)
         torch.cuda.synchronize()
         out[trail] = (reg, gm, dev.cpu().numpy())
     assert np.array_equal(out["1"][0], out["0"][0])
@@ -190,19 +186,3 @@ def test_trailing_rerun_of_flagged_batches(eng, monkeypatch):
     _lib.call("ocx_test_gT_regrets_unclean", 5, T, 0, runs, d, SQ2, _lib.ptr(got),
               eng.LANES_BEST, 0, 2)
     assert np.array_equal(got, ref)
-
-
-def test_trailing_d1024_best_layout(eng, monkeypatch):
-    """configs[4]'s shape under OCX_LANES_BEST: the trailing path takes the 64 x 16 layout where
-    the sequential loop keeps 32 x 32, so the two differ by the butterfly order's rounding only
-    (the closed-form bar), and the trailing regrets equal those of the sequential loop asked
-    for 64 x 16 bit for bit."""
-    _capacity_limited(monkeypatch, 0.1)
-    T, d, runs = 512, 1024, 90
-    monkeypatch.setenv("OCX_TRAILING", "1")
-    got = eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=eng.LANES_BEST)
-    monkeypatch.setenv("OCX_TRAILING", "0")
-    ref = eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=eng.LANES_BEST)
-    ref64 = eng.gT_regrets(T, runs, base_seed=9, d=d, lanes_per_seq=64)
-    assert np.array_equal(got, ref64)
-    assert close_closed(got, ref, T)
