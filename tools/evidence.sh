@@ -24,6 +24,7 @@
 #   overlaptrace rocprofv3 --kernel-trace of the overlapped pipeline (concurrency evidence)
 #   trail        tools/trail_probe.py (trailing pipeline vs sequential: configs[4], configs[3] T=1e5)
 #   trailtrace   rocprofv3 --kernel-trace of the trailing pipeline on the T = 1e5 case
+#   trailtraffic FETCH_SIZE / WRITE_SIZE of the trailing pipeline's kernels (tools/trail_traffic.py)
 #   genscale     tools/genscale_probe.py (d = 1024 generator time vs streams per SIMD)
 #   cumask       tools/cumask_map (CU-mask placement) and tools/cumask_probe.py (CU-split overlap)
 #   config3      tools/perf_extra.py config3 (configs[2]: FTRL vs exact FTL, generation included)
@@ -108,6 +109,13 @@ for step in "$@"; do
   trailtrace)
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_ttrace" -o tt --output-format csv -- python3 "$R/tools/trail_probe.py" --cases t1e5 --runs-t5 19600 --check 0 > "${O}_ttrace.log" 2>&1) || fail trailtrace $?
     ls "${O}_ttrace" ;;
+  trailtraffic)
+    # HBM bytes of the trailing pipeline on two T = 1e5 batches (9 800 runs), two PMC passes
+    for C in FETCH_SIZE WRITE_SIZE; do
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "${O}_tpmc_$C" -o pmc -- python3 "$R/tools/trail_probe.py" --cases t1e5 --runs-t5 9800 --only-trailing --check 0 > "${O}_tpmc_$C.log" 2>&1) || fail "trail pmc $C" $?
+    done
+    python tools/trail_traffic.py "${O}_tpmc_FETCH_SIZE" "${O}_tpmc_WRITE_SIZE" 9800 100000 > "${O}_trailtraffic.json" || fail trailtraffic $?
+    cat "${O}_trailtraffic.json" ;;
   genscale)
     timeout -k 10 300 python -u tools/genscale_probe.py > "${O}_genscale.jsonl" 2> "${O}_genscale.err" || fail genscale $?
     cat "${O}_genscale.jsonl" ;;

@@ -5,6 +5,7 @@ timesteps/s of engine.gT_max (what empirical_worst_case_thresholds runs per T), 
 call of the same shape, and whether the regrets equal the sequential loop's bit for bit.
 
     python tools/trail_probe.py [--cases c4,t1e5] [--chunks 8,4,16] [--runs-c4 32768] [--runs-t5 131072]
+                                [--check 0] [--only-trailing]
 """
 import argparse
 import json
@@ -27,6 +28,7 @@ def main():
     ap.add_argument("--runs-c4", type=int, default=32768)
     ap.add_argument("--runs-t5", type=int, default=131072)
     ap.add_argument("--check", type=int, default=1, help="compare regrets with the sequential loop")
+    ap.add_argument("--only-trailing", action="store_true", help="skip the sequential mode (PMC passes)")
     a = ap.parse_args()
     import torch
     from online_convex_optimization_amd import engine
@@ -34,7 +36,8 @@ def main():
         T, d = CASES[case]
         runs = a.runs_c4 if case == "c4" else a.runs_t5
         ref = None
-        modes = [("sequential", "0", None)] + [("trailing", "1", c) for c in a.chunks.split(",")]
+        modes = [] if a.only_trailing else [("sequential", "0", None)]
+        modes += [("trailing", "1", c) for c in a.chunks.split(",")]
         for name, trail, chunks in modes:
             os.environ["OCX_TRAILING"] = trail
             if chunks:
