@@ -425,7 +425,7 @@ PipeArgs pipe_args(const ocx_layout* L, const double* zt, const double* yt, doub
 
 // The pipelined step pays where one wave's step latency sets the batch time: the few-wave
 // butterfly layouts OCX_LANES_BEST chooses (8 x 8, 16 x 4 at d = 64; 16 x 16; 32 x 32 at
-// d = 1024) and their neighbours, and 64 x 16 at d = 1024 (lanes_per_seq = 64: 17.3 vs 19.2 ms
+// d = 1024) and their neighbours, and 64 x 16 at d = 1024 (lanes_per_seq = 64: 17.4 vs 19.2-19.7 ms
 // for the 32 x 32 layout's pass over 2 688 x 5 000 steps, profiles/r05_genscale.jsonl).  Other
 // butterfly layouts keep the plain kernel.
 bool ocx_pipe_supported(const ocx_layout* L) {

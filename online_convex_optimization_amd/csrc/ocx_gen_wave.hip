@@ -1188,6 +1188,19 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
 #pragma unroll
                         for (int i = 0; i < 16; ++i)
                             __builtin_nontemporal_store(ring[jb ^ (2u * i)] * scr, zp + i * kst);
+                    } else if (kSW && P == 64) {
+                        // the 64 x 16 layout (one sequence per wave): store i fills half i%2 of
+                        // plane i/2; its slot (l/2)·16 + l%2 + 2(i/2) + 512(i%2) maps to
+                        // rix = base ^ 2(i/2) + 512(i%2), base = ((l/2)·16 + l%2) ^ ((l/2) & 30):
+                        // no per-store index arithmetic, and the 32 lanes of each half read 32
+                        // distinct bank pairs
+                        const unsigned jb = ((unsigned)(lane >> 1) * 16u + (unsigned)(lane & 1)) ^
+                                            ((unsigned)(lane >> 1) & 30u);
+                        double* zp = zrow + lane;
+#pragma unroll
+                        for (int i = 0; i < 16; ++i)
+                            __builtin_nontemporal_store(ring[(jb ^ (2u * (unsigned)(i >> 1))) + 512u * (unsigned)(i & 1)] * scr,
+                                                        zp + (i >> 1) * kst + (i & 1) * 64);
                     } else if (P <= 32) {
                         double* zp = zrow + st1k.k0 * kst + st1k.w0;
 #pragma unroll
