@@ -185,8 +185,10 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * solved with cvxpy at :119-128)
  *     min_x ½ Σ_{i<n} |z_i·x − y_i|   s.t.  ||x||_norm <= 1   (norm 0 l2, 1 l1, 2 linf)
  * for any rows and labels (no regime: where the closed forms above do not apply), on device
- * by a primal log-barrier path (damped Newton, μ from 1 to 1e-10).  Where
- * the minimiser is not unique the path's limit, the analytic centre of the optimal face, is
+ * by a primal log-barrier path (damped Newton, μ from 1 to 1e-10), then a
+ * polish: the active rows and face found at several thresholds, x purified onto them and the
+ * dual rebuilt from the KKT system, kept where it tightens the certificate.  Where the
+ * minimiser is not unique the path's limit, the analytic centre of the optimal face, is
  * returned.  Problems: each sequence's prefixes n = 0..T (all_prefixes = 1, actions
  * [B][T+1][d] as compute_prefix_actions :280-303 returns; actions[b][0] = 0) or n = T only
  * (all_prefixes = 0, [B][1][d]: the comparator).  obj [B][NP] (nullable) = ½Σ|r| at x
@@ -201,7 +203,7 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  *     centred step produces) at the last centre, after (info & 0xFFFFF) steps — accurate to
  *     that μ only.
  * Only a converged solve is an answer by itself; for the other two the certificate decides
- * (the engine accepts a solve iff info >= 0 and gap <= 1e-4·(1 + |obj|), and raises
+ * (the engine accepts a solve iff info >= 0 and gap <= 1e-8·(1 + |obj|), and raises
  * otherwise, as exact_ftl.py:125-126 does on a solver failure).  1 <= d <=
  * OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy: unpinned (validated
  * against scipy's HiGHS LPs and by the certificate). */

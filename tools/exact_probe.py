@@ -45,7 +45,7 @@ def main():
         worst = {"b": int(wb), "slot": int(wn), "gap": float(gap[wb, wn]), "obj": float(obj[wb, wn]),
                  "info": int(info[wb, wn]),
                  "x": g["actions"][wb, wn].cpu().numpy().tolist(),
-                 "n_gap_over_1e-4": int((gap > 1e-4 * (1 + obj)).sum())}
+                 "n_gap_over_1e-8": int((gap > 1e-8 * (1 + obj)).sum())}
         print(json.dumps({"B": B, "T": T, "d": d, "norm": norm, "all_prefixes": allp,
                           "problems": int(nprob), "kernel_ms": ms,
                           "problems_per_s": nprob / (ms * 1e-3),
