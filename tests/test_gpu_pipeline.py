@@ -186,3 +186,22 @@ def test_trailing_rerun_of_flagged_batches(eng, monkeypatch):
     _lib.call("ocx_test_gT_regrets_unclean", 5, T, 0, runs, d, SQ2, _lib.ptr(got),
               eng.LANES_BEST, 0, 2)
     assert np.array_equal(got, ref)
+
+
+def test_trailing_full_size_t1e5(eng):
+    """configs[3]'s T = 1e5 point at its full per-batch size (d = 64, the default HBM budget:
+    ≈4 500 runs per batch, 3 batches, the last smaller): the trailing path's regrets for
+    sequences of the first, middle and last batch within the closed-form bar of the oracle,
+    and g(T) equal to the max of the regrets the same call returns."""
+    import torch
+    T, d, runs = 100000, 64, 9800
+    reg = eng.gT_regrets(T, runs, base_seed=0, d=d, lanes_per_seq=eng.LANES_BEST)
+    gm = eng.gT_max(T, runs, base_seed=0, d=d, lanes_per_seq=eng.LANES_BEST)
+    assert gm == eng.max_regret(reg)
+    picks = [0, runs // 2, runs - 1]
+    zs, ys = zip(*(O.gT_sample(0, T, r, d) for r in picks))
+    ref = O.simulate_alg_batch(np.stack(zs), np.stack(ys), 0, SQ2, nthreads=3)[0]
+    for i, r in enumerate(picks):
+        assert close_closed(reg[r], ref[i], T), (r, reg[r], ref[i])
+    eng.release_buffers()
+    torch.cuda.empty_cache()
