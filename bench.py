@@ -152,6 +152,50 @@ def cpu_baseline_all_cores(T, d, budget_s, threads):
     return steps / spent, threads, n, spent
 
 
+def cpu_leg(a, T, d, B, regrets):
+    """The CPU baseline (oracle/ocx_oracle.c on this host's cores) and the parity check of
+    rank 0's regrets against it.  Rank 0 runs it after the timed region at every world size
+    (the other ranks wait at the closing barrier, so no timed step overlaps it).  Returns
+    (cpu_baseline, parity)."""
+    cregs, cps, spent = cpu_baseline(T, d, B, a.cpu_seconds)
+    err = np.abs(regrets[:len(cregs)] - cregs)
+    # the closed-form comparator differs from the reference's sequential sum by
+    # that sum's own rounding (tests/test_gpu_parity.py close_closed)
+    tol = np.maximum(1e-12 * np.maximum(1.0, np.abs(cregs)), 4 * 2.22e-16 * T ** 1.5)
+    parity = {"n_checked": int(len(cregs)), "max_abs_err": float(err.max()),
+              "max_rel_err": float((err / np.maximum(np.abs(cregs), 1e-300)).max()),
+              "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs)),
+              "within_tolerance": bool(np.all(err <= tol)),
+              "tolerance": "max(1e-12*max(1,|ref|), 4*eps*T^1.5); north star 1e-6 rel"}
+    hc = host_cpu()
+    # every core of the affinity mask; and, when the cgroup's CPU quota is smaller,
+    # that many threads too (256 threads on a 16-CPU quota time-slice and run slower
+    # than 16): the better of the two is the all-cores baseline
+    legs = {}
+    aff = hc["affinity"] or os.cpu_count()
+    legs[aff] = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 6), aff)
+    quota = cgroup_cpu_quota()
+    if quota is not None and int(quota) < aff:
+        q = max(1, int(quota))
+        legs[q] = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 6), q)
+    acps, threads, nseq, aspent = max(legs.values(), key=lambda v: v[0])
+    cpu = {"value": cps, "unit": "timesteps/s", "cores": 1, "kind": "port",
+           "sample": f"{len(cregs)} sequences of the same workload (d={d}, T={T}, "
+                     f"runs 0..{len(cregs) - 1}), oracle/ocx_oracle.c (gcc -O3 "
+                     f"-ffp-contract=off) single thread, {spent:.1f} s",
+           "cpu_model": hc["model"], "host_nproc": hc["nproc"],
+           "host_affinity": hc["affinity"],
+           "value_all_cores": acps, "cores_all": threads,
+           "cores_all_source": "OpenMP threads passed explicitly (OMP_NUM_THREADS not "
+                               "honoured): the better of len(os.sched_getaffinity(0)) "
+                               "and the cgroup CPU quota",
+           "cgroup_cpu_quota": cgroup_cpu_quota(),
+           "all_cores_by_threads": {str(k): v[0] for k, v in legs.items()},
+           "sample_all_cores": f"{nseq} sequences ({nseq // threads} per OpenMP "
+                               f"thread), runs 0..{nseq - 1}, {aspent:.1f} s"}
+    return cpu, parity
+
+
 def host_cpu():
     """CPU model and core counts of the host this bench runs on."""
     model = None
@@ -184,16 +228,20 @@ def device_identity(gpu: int) -> dict:
 
 
 def rank_report(dist, rank: int, world: int, ident: dict, elapsed_s: float, kern_ms: float,
-                regrets: np.ndarray, gathered: np.ndarray) -> dict:
+                regrets: np.ndarray, gathered: np.ndarray, alg_bytes: float = None) -> dict:
     """The multi-rank self-check printed with the bench line (collective: every rank calls
     it).  Every rank contributes its identity, its own wall time over the timed steps, its
     kernel time and a checksum of its own regrets (all_gather_object); rank 0 then checks
     each rank's block of the gathered regret vector against that rank's checksum, so the
     line shows that N distinct GPUs ran N disjoint shards and that the collective moved
-    them intact."""
+    them intact.  With `alg_bytes` (this rank's algorithmic bytes per launch) each rank also
+    reports its own roofline fraction."""
     regrets = np.asarray(regrets, dtype=np.float64)
+    frac = None
+    if alg_bytes is not None and kern_ms > 0:
+        frac = float(alg_bytes) / (kern_ms * 1e-3) / 1e9 / PEAK_HBM_GBS
     mine = dict(ident, rank=int(rank), elapsed_ms=float(elapsed_s) * 1e3,
-                kernel_ms=float(kern_ms), n_regrets=int(regrets.size),
+                kernel_ms=float(kern_ms), frac=frac, n_regrets=int(regrets.size),
                 regret_sum=float(np.sum(regrets)), regret_sumsq=float(np.sum(regrets * regrets)))
     rows = [None] * world
     dist.all_gather_object(rows, mine)
@@ -216,19 +264,51 @@ def free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def launch_ranks(n: int, argv, script: str = None) -> int:
+def launch_ranks(n: int, argv, script: str = None, timeout_s: float = None) -> int:
     """`bench.py --gpus N` without a launcher: run `script` (this file) as N ranks of one
-    node through torch.distributed.run, in a child process, and return its exit status.
-    The parent never initialises a GPU (it only parses arguments), so nothing is exec'd
-    from a process holding a HIP context; each rank reads RANK / LOCAL_RANK / WORLD_SIZE /
-    MASTER_* from the environment torchrun gives it, and rank 0 prints the line."""
+    node, each a child process with the environment torchrun would give it (RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1, MASTER_PORT), and
+    return the first non-zero exit status (0 when every rank succeeded).  The ranks are
+    started directly rather than through torch.distributed.run, whose own argument parser
+    takes prefixes of the script's options for its own (`--d` is ambiguous there).  The
+    parent only parses arguments and counts the visible devices (torch.cuda.device_count(),
+    which creates no HIP context on this image), and it never execs: the ranks are children.
+    If a rank fails, the others are terminated (they would wait for it at the rendezvous)."""
     import subprocess
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={int(n)}", "--master-addr=127.0.0.1",
-           f"--master-port={free_port()}", script or os.path.abspath(__file__), *argv]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
-    return subprocess.call(cmd, env=env)
+    port = free_port()
+    procs = []
+    for r in range(int(n)):
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(int(n)),
+                   LOCAL_WORLD_SIZE=str(int(n)), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__),
+                                       *argv], env=env))
+    t_end = None if timeout_s is None else time.monotonic() + timeout_s
+    status = [None] * len(procs)
+    while any(s is None for s in status):
+        for i, p in enumerate(procs):
+            if status[i] is None:
+                status[i] = p.poll()
+        bad = [s for s in status if s not in (None, 0)]
+        late = t_end is not None and time.monotonic() > t_end
+        if bad or late:
+            for i, p in enumerate(procs):
+                if status[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if status[i] is None:
+                    try:
+                        status[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        status[i] = p.wait()
+            if late and not bad:
+                return 124
+            break
+        time.sleep(0.05)
+    return next((s for s in status if s != 0), 0)
 
 
 def rank_env(a, device_count: int):
@@ -242,8 +322,11 @@ def rank_env(a, device_count: int):
     if launched and world != a.gpus:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         raise SystemExit(2)
-    if a.dist_backend == "nccl" and device_count < world:
-        print(f"bench.py: {world} ranks need {world} GPUs, {device_count} visible",
+    # the ranks of THIS node need one device each (a multi-node launch has WORLD_SIZE above
+    # one node's device count)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if a.dist_backend == "nccl" and (device_count < local_world or local >= device_count):
+        print(f"bench.py: {local_world} local ranks need {local_world} GPUs, {device_count} visible",
               file=sys.stderr)
         raise SystemExit(2)
     gpu = local % max(1, device_count) if a.dist_backend == "gloo" else local
@@ -422,19 +505,19 @@ def main():
         db.simulate_alg(0, math.sqrt(2), closed_comparator=closed)
 
     regrets = db.regret[:B].cpu().numpy()
+    # one pass over z per sequence, a second one for the waves that streamed it
+    alg_bytes = (B + seq_pass2) * T * (8 * d + 8)
     ranks = None
     if dist_on:
         # the regret vector of the last timed step (the e2e batches regenerate the same runs)
         gather()
         torch.cuda.synchronize()
         ranks = rank_report(dist, rank, world, device_identity(gpu), elapsed, kern_ms, regrets,
-                            gathered.cpu().numpy())
+                            gathered.cpu().numpy(), alg_bytes)
     out = None
     if rank == 0:
         steps_per_launch = B * T
         value = world * B * T * a.steps / elapsed
-        # one pass over z per sequence, a second one for the waves that streamed it
-        alg_bytes = (B + seq_pass2) * T * (8 * d + 8)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         try:
@@ -447,45 +530,9 @@ def main():
                 traffic = tr.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
-        cpu = None
-        parity = None
-        if a.cpu_seconds > 0 and world == 1:  # the CPU leg: rank 0 at N = 1 only
-            cregs, cps, spent = cpu_baseline(T, d, B, a.cpu_seconds)
-            err = np.abs(regrets[:len(cregs)] - cregs)
-            # the closed-form comparator differs from the reference's sequential sum by
-            # that sum's own rounding (tests/test_gpu_parity.py close_closed)
-            tol = np.maximum(1e-12 * np.maximum(1.0, np.abs(cregs)), 4 * 2.22e-16 * T ** 1.5)
-            parity = {"n_checked": int(len(cregs)), "max_abs_err": float(err.max()),
-                      "max_rel_err": float((err / np.maximum(np.abs(cregs), 1e-300)).max()),
-                      "bitexact": bool(np.array_equal(regrets[:len(cregs)], cregs)),
-                      "within_tolerance": bool(np.all(err <= tol)),
-                      "tolerance": "max(1e-12*max(1,|ref|), 4*eps*T^1.5); north star 1e-6 rel"}
-            hc = host_cpu()
-            # every core of the affinity mask; and, when the cgroup's CPU quota is smaller,
-            # that many threads too (256 threads on a 16-CPU quota time-slice and run slower
-            # than 16): the better of the two is the all-cores baseline
-            legs = {}
-            aff = hc["affinity"] or os.cpu_count()
-            legs[aff] = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 6), aff)
-            quota = cgroup_cpu_quota()
-            if quota is not None and int(quota) < aff:
-                q = max(1, int(quota))
-                legs[q] = cpu_baseline_all_cores(T, d, max(2.0, a.cpu_seconds / 6), q)
-            acps, threads, nseq, aspent = max(legs.values(), key=lambda v: v[0])
-            cpu = {"value": cps, "unit": "timesteps/s", "cores": 1, "kind": "port",
-                   "sample": f"{len(cregs)} sequences of the same workload (d={d}, T={T}, "
-                             f"runs 0..{len(cregs) - 1}), oracle/ocx_oracle.c (gcc -O3 "
-                             f"-ffp-contract=off) single thread, {spent:.1f} s",
-                   "cpu_model": hc["model"], "host_nproc": hc["nproc"],
-                   "host_affinity": hc["affinity"],
-                   "value_all_cores": acps, "cores_all": threads,
-                   "cores_all_source": "OpenMP threads passed explicitly (OMP_NUM_THREADS not "
-                                       "honoured): the better of len(os.sched_getaffinity(0)) "
-                                       "and the cgroup CPU quota",
-                   "cgroup_cpu_quota": cgroup_cpu_quota(),
-                   "all_cores_by_threads": {str(k): v[0] for k, v in legs.items()},
-                   "sample_all_cores": f"{nseq} sequences ({nseq // threads} per OpenMP "
-                                       f"thread), runs 0..{nseq - 1}, {aspent:.1f} s"}
+        cpu, parity = None, None
+        if a.cpu_seconds > 0:  # rank 0, every world size, after the timed region
+            cpu, parity = cpu_leg(a, T, d, B, regrets)
         out = {
             "metric": "FTRL timesteps/sec (whole node) at d=64, T=1e4; max |regret-ref| error",
             "value": value,

@@ -35,6 +35,10 @@ int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const 
                               double eta0, int64_t chunk_steps, double* regret, int* bad,
                               void* stream);
 
+/* Batches that have entered the trailing pipeline (ocx_run_gen_sim_trailing) in this process
+ * so far: lets a test assert that a call took that path rather than the sequential loop. */
+int64_t ocx_test_trailing_batches(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -114,6 +114,7 @@ TEST_SIGNATURES = {
                                             c_int, c_int, c_i64]),
     "ocx_test_alg_pipe_chunked": (c_int, [ctypes.POINTER(Layout), c_vp, c_vp, c_double, c_i64,
                                           c_vp, c_vp, c_vp]),
+    "ocx_test_trailing_batches": (c_i64, []),
 }
 OCX_VERSION = 400  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1

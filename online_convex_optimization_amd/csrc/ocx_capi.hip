@@ -1231,6 +1231,8 @@ int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const 
     return OCX_OK;
 }
 
+int64_t ocx_test_trailing_batches(void) { return ocx_trailing_batches_run(); }
+
 int ocx_test_gT_regrets_unclean(uint64_t base_seed, int64_t T, int64_t run0, int64_t R,
                                 int64_t d, double eta0, double* regrets, int lanes_per_seq,
                                 int device, int64_t unclean_every) {

@@ -418,7 +418,8 @@ namespace {
 // interpolates rows (n > d real-valued rows: an LAD vertex; n < d rows fitted exactly) the
 // barrier certificate stayed near 1e-5 relative, and a zero-loss prefix kept ½Σ|r_i| ≈ 5e-8.
 // For each of seven threshold scales (the best is kept; every bound is valid):
-//   1. active set at x: rows with |r_i| <= τ_r (1 + |y_i|) (at most 63), and the ball's
+//   1. active set at x: rows with |r_i| <= τ_r (1 + |y_i|) (at most 64, 63 beside the cone
+//      row), and the ball's
 //      constraints that hold: l2 ||x|| = 1; linf |x_j| = 1 (those coordinates fixed at ±1);
 //      l1 ||x||_1 = 1 (the zero coordinates fixed at 0, the others keep their signs);
 //   2. primal purification: the least-change step δ (minimum norm over the free coordinates)
@@ -471,11 +472,15 @@ __device__ void polish_cholesky_solve(double* K, double* sc, int lane, double rh
     lds_sync();
 }
 
+// The bar under which the polish keeps the solver's own x: a decade inside the host's
+// acceptance bar (engine.EXACT_GAP_RTOL = 1e-8), so a kept x always passes it.
+constexpr double kKeepRtol = 1e-9;
+
 template <int NORM>
 __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
     WideSrc rs, int64_t B, int64_t NP, int64_t p0, double* __restrict__ actions,
     double* __restrict__ obj, double* __restrict__ gap, double* __restrict__ step_loss) {
-    constexpr int DP = 64, LD = DP + 1, AM = 63;
+    constexpr int DP = 64, LD = DP + 1;
     extern __shared__ double lds[];
     double* M = lds;             // [64][LD] the active rows (+ the cone row)
     double* K = M + DP * LD;     // [64][LD] staged rows during passes; the small systems
@@ -501,6 +506,9 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
     const double x = cj ? actions[o * d + lane] : 0.0;
     double best = g0, pbest = f0, xbest = x;
     bool improved = false;
+    // the certificate of the solver's own x (P(x) - D, valid for any dual of the box): where it
+    // passes, x — the path's analytic-centre limit ocx.h promises — is kept, not x'
+    double bestx = g0, P0x = f0;
 
     // stage rows [c0, c0 + rows) into K; y into yv (lane r)
     auto stage = [&](int64_t c0, int rows, double& yv) {
@@ -540,6 +548,9 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
             }
         }
         const bool freec = cj && !fixed;
+        // active rows the [64][65] systems hold: 64, one fewer beside the cone row (d = 64: an
+        // LAD vertex inside the ball interpolates 64 rows)
+        const int AM = DP - (cone ? 1 : 0);
         const double vfix = fixed ? tgt - x : 0.0;  // δ_j on a fixed coordinate
         lds_sync();
         xs[lane] = x;
@@ -571,6 +582,7 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
         }
         if (over) continue;  // wave-uniform: too many active rows at this scale
         P0 = wsum(P0);
+        P0x = P0;
         const int mr = m + (cone ? 1 : 0);
         lds_sync();
         // ---- 2. primal purification: rows of the active set (+ the cone row) into M
@@ -697,13 +709,22 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
             nw = mx;
         }
         const double gn = fmax(P1 - (-Y - nw), 0.0);
+        bestx = fmin(bestx, fmax(P0 - (-Y - nw), 0.0));
         if (gn < best) {
             best = gn;
             pbest = P1;
             xbest = xn;
             improved = true;
         }
-        if (best <= 1e-14 * (1.0 + pbest)) break;  // to rounding: done
+        if (best <= 1e-14 * (1.0 + pbest) && bestx <= kKeepRtol * (1.0 + fabs(P0x))) break;
+    }
+    if (bestx < g0 && bestx <= kKeepRtol * (1.0 + fabs(P0x))) {
+        // x certifies on its own: keep it (and its step loss), report its objective and gap
+        if (lane == 0) {
+            obj[o] = P0x;
+            gap[o] = bestx;
+        }
+        return;
     }
     if (!improved) return;
     if (cj) actions[o * d + lane] = xbest;

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -304,6 +305,10 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L) {
     return b;
 }
 
+// batches that have entered the trailing pipeline in this process (ocx_test_trailing_batches)
+static std::atomic<int64_t> g_trailing_batches{0};
+int64_t ocx_trailing_batches_run() { return g_trailing_batches.load(); }
+
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,
@@ -312,6 +317,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
     if (!ocx_trailing_supported(L) || nbatch <= 0 || !regret || !gst || !fst || !bad ||
         last_B < 1 || last_B > L->B)
         return hipErrorInvalidValue;
+    g_trailing_batches += nbatch;
     ocx_layout Ll = *L;  // the last batch: same tiles, last_B runs
     Ll.B = last_B;
     auto lay = [&](int64_t k) { return k + 1 == nbatch ? &Ll : L; };

@@ -62,6 +62,7 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 bool ocx_trailing_supported(const ocx_layout* L);
 // the largest batch whose generator waves all fit beside the FTRL chunks' waves
 int64_t ocx_trailing_max_batch(const ocx_layout* L);
+int64_t ocx_trailing_batches_run();  // batches through ocx_run_gen_sim_trailing so far
 hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int64_t run0,
                                     int64_t nbatch, double* zt, double* yt0, double* yt1,
                                     uint64_t* gst, double* fst, int* bad, double eta0,

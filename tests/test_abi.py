@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols(header="ocx.h"):
     with open(os.path.join(ROOT, "include", header)) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"^\s*int\s+(ocx_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t)\s+(ocx_\w+)\s*\(", txt, flags=re.M)))
 
 
 @pytest.mark.parametrize("header,table", [("ocx.h", "SIGNATURES"),

@@ -338,10 +338,11 @@ def test_tied_prefixes_take_the_general_solvers_centre(eng, norm):
 
 
 @pytest.mark.parametrize("norm", ["linf", "l1", "l2"])
-@pytest.mark.parametrize("d", [5, 11, 33])
+@pytest.mark.parametrize("d", [5, 11, 33, 64])
 def test_interpolating_optimum_certifies(eng, norm, d):
     """n > d unclipped rows (3·N(0,1)) with real-valued labels: the optimum interpolates rows
-    exactly (a vertex of the LAD fit), where the barrier's multipliers of those rows are only
+    exactly (a vertex of the LAD fit; at d = 64 inside the ball it interpolates 64 rows, the
+    most the polish's active set holds), where the barrier's multipliers of those rows are only
     as good as μ_end (their certificate stayed near 1e-5 relative).  The polished dual
     (ocx_exact_polish_kernel: ±½ on the other rows, least squares on stationarity for the
     interpolated ones) certifies every prefix to 1e-8·(1 + obj), and it is a valid bound."""

@@ -147,22 +147,29 @@ def _capacity_limited(monkeypatch, gb):
 
 
 @pytest.mark.parametrize("T,d,runs,gb,chunks", [(2000, 64, 1000, 0.35, "8"), (700, 64, 900, 0.06, "3"),
-                                                (640, 1024, 130, 0.25, "4"), (300, 64, 500, 0.02, "2")])
+                                                (300, 64, 500, 0.02, "2"), (200, 64, 9000, 0.5, "2")])
 def test_trailing_equals_sequential(eng, monkeypatch, T, d, runs, gb, chunks):
     """Regrets (host and device-resident) and g(T) of the trailing path equal the sequential
     loop's bit for bit, over several batches and a smaller last one, and sampled sequences are
-    within the closed-form bar of the oracle."""
+    within the closed-form bar of the oracle.  The first three cases' batches (< 4 096 runs)
+    take the 16 x 4 layout, the last one's (4 500 runs) 8 x 8; each call is checked to have
+    gone through the trailing pipeline (ocx_test_trailing_batches)."""
     import torch
+    from online_convex_optimization_amd import _lib
     _capacity_limited(monkeypatch, gb)
     monkeypatch.setenv("OCX_TRAIL_CHUNKS", chunks)
     out = {}
     for trail in ("0", "1"):
         monkeypatch.setenv("OCX_TRAILING", trail)
+        n0 = _lib.load().ocx_test_trailing_batches()
         reg = eng.gT_regrets(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
         gm = eng.gT_max(T, runs, base_seed=3, d=d, run0=11, lanes_per_seq=eng.LANES_BEST)
         dev = eng.gT_regrets_device(T, runs, base_seed=3, d=d, run0=11,
                                     lanes_per_seq=eng.LANES_BEST)
         torch.cuda.synchronize()
+        ran = _lib.load().ocx_test_trailing_batches() - n0
+        # three calls, two or more batches each through the trailing path (none without it)
+        assert (ran >= 6) if trail == "1" else (ran == 0), (trail, ran)
         out[trail] = (reg, gm, dev.cpu().numpy())
     assert np.array_equal(out["1"][0], out["0"][0])
     assert out["1"][1] == out["0"][1] == eng.max_regret(out["0"][0])
