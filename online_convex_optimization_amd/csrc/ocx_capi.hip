@@ -990,6 +990,31 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
                 }
             }
         }
+        // Full generator waves (round 6): where the generator runs one wave per stream in a
+        // single round (d = 1024: the HBM budget holds ~3 000 streams, the form 4 096 resident
+        // waves) a batch takes as long as its busiest SIMD's waves, ceil(chunk / SIMDs), and
+        // the d = 1024 and d = 64 forms cost the same per row at equal waves per SIMD (1 / 2 / 3
+        // waves: 988 / 567 / 495 vs 1 106 / 610 / 495 cycles per 64-normal row,
+        // profiles/r06_genwaves.jsonl).  So batches of whole waves per SIMD (a multiple of the
+        // SIMDs, the last one the remainder) replace equal ones when that needs fewer waves in
+        // all: 32 768 runs as 10 x 3 072 + 2 048 (32 waves per SIMD) instead of 12 x 2 731 (36).
+        // OCX_BATCH_WAVES=0: equal batches (tuning).
+        if (d != 64 && R > chunk) {
+            const char* bw = std::getenv("OCX_BATCH_WAVES");
+            int dev = 0, cus = 256;
+            OCX_HIP(hipGetDevice(&dev));
+            OCX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            const int64_t simds = 4 * (int64_t)cus;
+            const int64_t cap = std::max<int64_t>(64, std::min<int64_t>(budget / per_seq, R));
+            const int64_t cw = cap / simds * simds;
+            if ((!bw || std::atoi(bw) != 0) && cw >= simds && cw <= ocx_gen_resident_waves(d, dev)) {
+                auto waves = [simds](int64_t n) { return (n + simds - 1) / simds; };
+                const int64_t nb = (R + chunk - 1) / chunk;
+                const int64_t eq = (nb - 1) * waves(chunk) + waves(R - (nb - 1) * chunk);
+                const int64_t full = (R / cw) * (cw / simds) + waves(R % cw);
+                if (full < eq) chunk = cw;
+            }
+        }
         OCX_HIP(cx->out.ensure((size_t)chunk * 8));
         // Generation overlapped with FTRL (ocx_pipeline.hip) where the layout allows it
         // (OCX_PIPELINE=0: the sequential loop below).  For g(T) alone the equal batches go

@@ -786,6 +786,37 @@ __device__ __forceinline__ double leaf_sumsq(const double* ring, int rmask, unsi
     return res;
 }
 
+// The sums of squares of a batch of 512 ring normals = 512/DF rows of DF = 16 or 32 normals
+// (the small-d rows, rows r at ring[r·DF, (r+1)·DF)): DF/8 lanes per row, every lane keeping
+// 8/(DF/8) of NumPy's eight accumulators r_k = Σ_q v_{k+8q}² (8 loads per lane), summed in the
+// lane as the left or right part of ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) and combined across
+// the row's lanes by the butterfly ocx_seq_sum<DF/8>: the pairwise order of a leaf of DF <= 128
+// elements, bit for bit.  Lane l serves row l / (DF/8); every lane of the row gets the sum.
+template <int DF>
+__device__ __forceinline__ double batch_sumsq_small(const double* ring, int lane) {
+    static_assert(DF == 16 || DF == 32, "small-d batch rows");
+    constexpr int LPR = DF / 8;   // lanes per row
+    constexpr int K = 8 / LPR;    // accumulators per lane
+    constexpr int Q = DF / 8;     // terms per accumulator
+    const int row = lane / LPR, c = lane % LPR;
+    const double* rp = ring + row * DF + c * K;
+    double r[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const double v0 = rp[i];
+        r[i] = v0 * v0;
+#pragma unroll
+        for (int q = 1; q < Q; ++q) {
+            const double v = rp[i + 8 * q];
+            r[i] += v * v;
+        }
+    }
+    double part;
+    if constexpr (K == 4) part = (r[0] + r[1]) + (r[2] + r[3]);
+    else part = r[0] + r[1];
+    return ocx_seq_sum<LPR>(part);
+}
+
 // np.linalg.norm(z, axis=1)**2 for one row of d values (pairwise_sum recursion above
 // 128 elements: split at n/2 rounded down to a multiple of 8, left + right).  The
 // post-order walk of that recursion keeps its (uniform) stack in the wave's LDS slot
@@ -870,7 +901,7 @@ __host__ __device__ constexpr int gen_block(int DF, bool LR, int OV = 0) {
 // wave) and tables (6 KB per block) admit six waves per SIMD in LDS; the default form keeps
 // the four-wave register budget (no spills), the few-stream form (LR) asks for six.
 #ifndef OCX_GENW_MIN_WAVES
-#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? 4 : 1))
+#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : (((DF) == 1024 || (DF) == 16 || (DF) == 32) ? 4 : 1))
 #else
 #define OCX_GENW_MIN_WAVES_FOR(DF, LR) OCX_GENW_MIN_WAVES
 #endif
@@ -925,8 +956,10 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
     constexpr int kBlock = gen_block(DF, LR, OV);
     constexpr int kNW = kBlock / 64;
     // lane states in the round loop: the d = 64 row loop's FLAT rounds (see zig_round)
-    constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 && (DF == 64 || (DF == 1024 && OCX_GEN_1K_FLAT));
-    constexpr bool kKD = OCX_GEN_KI_DOUBLE && DF == 64;  // ki as doubles (see ZigTables)
+    constexpr bool kSmall = DF == 16 || DF == 32;  // the small-d rows (the d = 64 loop's form)
+    constexpr bool kLS = OCX_GEN_LANE_STATE && MODE == 0 &&
+                         (DF == 64 || kSmall || (DF == 1024 && OCX_GEN_1K_FLAT));
+    constexpr bool kKD = OCX_GEN_KI_DOUBLE && (DF == 64 || kSmall);  // ki as doubles (see ZigTables)
     constexpr bool kDF = OCX_GEN_DEFER && MODE == 0 && DF == 64 && !LR && OCX_GEN_INNER;  // deferred wedges
     __shared__ ZigTables<kKD> tb;
     extern __shared__ double rings[];
@@ -959,7 +992,7 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
     w.Ak = ((ocx_u128)kJumpTable.w[lane][1] << 64) | kJumpTable.w[lane][0];
     const int d = DF ? DF : d_arg;
     const int S = 64 / P;
-    const int Dp = DF == 64 ? 64 : P * C;
+    const int Dp = (DF == 64 || kSmall) ? DF : P * C;
     // DF = 1024 store map: flat index f = i*64 + lane of the row → plane k = f / (2P),
     // offset w = f % (2P) of the sequence's segment in that plane, coordinate
     // j = (w/2)*C + 2k + (w%2)
@@ -1050,7 +1083,10 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
         ws_set<kLS>(w, g0, Gk);
 
         // ---- rows
-        if constexpr (MODE == 0 && DF == 64) {
+        if constexpr (MODE == 0 && (DF == 64 || DF == 32 || DF == 16)) {
+            // DF = 16 / 32 (round 6): the same loop over batches of 512 normals = 512/DF rows
+            // (32 / 16), their sums of squares by batch_sumsq_small (DF/8 lanes per row), the
+            // stores 64/DF rows per pass.  The notes below are the d = 64 form's.
             // d = 64, a front-moving ring of R rows + one round (kRows64 * 64 + 64 doubles):
             // rows always start at ring[0], so no index is ever masked and every ring access
             // is a fixed base + an immediate offset.  A batch of R rows leaves as soon as the
@@ -1058,20 +1094,21 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             // move to the front (LDS operations of a wave run in order: the batch's reads come
             // first); the last batch may be shorter.  The batch's row scales reach the store
             // lanes through LDS (`scl`, one broadcast read per row) instead of readlanes.
-            constexpr int RR = kRows64;
-            const uint32_t total = (uint32_t)(nrows * 64);
+            constexpr int RR = DF == 64 ? kRows64 : 512 / DF;  // rows per batch (512 normals)
+            constexpr int kRP = 64 / DF;                      // rows per store pass
+            const uint32_t total = (uint32_t)(nrows * DF);
             uint32_t produced = 0;
             unsigned head = 0;  // normals in the ring
             int64_t t = t_off;
-            double* scl = ring + RR * 64 + 64;  // the batch's row scales
+            double* scl = ring + RR * DF + 64;  // the batch's row scales
             // deferred wedges (the default form): the pending list and the removed-slot flags
             // follow the scales in the wave's slot (ring_doubles)
-            uint64_t* pend = reinterpret_cast<uint64_t*>(ring + RR * 64 + 64 + 8);
-            unsigned char* gone = reinterpret_cast<unsigned char*>(ring + RR * 64 + 64 + 8 + 2 * kPendMax);
+            uint64_t* pend = reinterpret_cast<uint64_t*>(ring + RR * DF + 64 + 8);
+            unsigned char* gone = reinterpret_cast<unsigned char*>(ring + RR * DF + 64 + 8 + 2 * kPendMax);
             int npend = 0;
             while (produced < total) {
 #if OCX_GEN_INNER
-                if (total - produced >= (uint32_t)(RR * 64 + 64)) {
+                if (total - produced >= (uint32_t)(RR * DF + 64)) {
                     // a whole batch still to draw: full rounds until the ring holds it, with
                     // one loop test per round (no per-round need / last-round / batch tests;
                     // every round here has 64 or more normals left to draw — with deferred
@@ -1085,13 +1122,13 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
 #if OCX_GEN_UNROLL == 2
                         // two rounds per trip: the state alternates between two register sets
                         // (no back-edge copies of the 128-bit lane states)
-                        if (head >= (unsigned)(RR * 64) || (kDF && npend >= kPendFlush)) break;
+                        if (head >= (unsigned)(RR * DF) || (kDF && npend >= kPendFlush)) break;
                         const int n2 = zig_round<true, true, true, 0, false, kDF>(w, 64, tb, ring, 0, head,
                                                                                  lane, pend, &npend);
                         produced += (uint32_t)n2;
                         head += (unsigned)n2;
 #endif
-                    } while (head < (unsigned)(RR * 64) && !(kDF && npend >= kPendFlush));
+                    } while (head < (unsigned)(RR * DF) && !(kDF && npend >= kPendFlush));
                     if constexpr (kDF) resolve_wedges(ring, pend, gone, npend, head, produced, tb, lane);
                 } else
 #endif
@@ -1104,24 +1141,41 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
                     produced += (uint32_t)n;
                     head += (unsigned)n;
                 }
-                if (head >= (unsigned)(RR * 64) || (produced == total && head > 0)) {
-                    const int nrows = (int)(head >> 6) < RR ? (int)(head >> 6) : RR;
-                    // lanes 8r..8r+7: row r's NumPy pairwise sum of squares, its clip scale
-                    const double ss = leaf_sumsq<64>(ring, -1, (unsigned)((lane >> 3) * 64), 64, lane);
+                if (head >= (unsigned)(RR * DF) || (produced == total && head > 0)) {
+                    const int nrows = (int)(head / DF) < RR ? (int)(head / DF) : RR;
+                    // lanes 8r..8r+7 (DF/8 lanes per row at DF < 64): row r's NumPy pairwise sum
+                    // of squares, its clip scale
+                    double ss;
+                    if constexpr (DF == 64) ss = leaf_sumsq<64>(ring, -1, (unsigned)((lane >> 3) * 64), 64, lane);
+                    else ss = batch_sumsq_small<DF>(ring, lane);
                     const double nrm = sqrt(ss);
                     const double sc = 1.0 / (nrm > 1.0 ? nrm : 1.0);  // 1.0 / np.maximum(norms, 1.0)
-                    scl[lane >> 3] = sc;  // the 8 lanes of a row write the same value
+                    scl[lane / (DF / 8)] = sc;  // the lanes of a row write the same value
                     double* zp = zt + zoff + t * 128;
-                    // lane j stores coordinate j of each row
-                    if (nrows == RR) {
+                    if constexpr (DF == 64) {
+                        // lane j stores coordinate j of each row
+                        if (nrows == RR) {
 #pragma unroll
-                        for (int r = 0; r < RR; ++r)
-                            OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
+                            for (int r = 0; r < RR; ++r)
+                                OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
+                        } else {
+                            for (int r = 0; r < nrows; ++r)
+                                OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
+                        }
                     } else {
-                        for (int r = 0; r < nrows; ++r)
-                            OCX_GEN_STORE(ring[64 * r + lane] * scl[r], zp + r * 128);
+                        // pass i: lane l stores coordinate l % DF of row i·kRP + l / DF
+                        zp += rl * 128;
+                        if (nrows == RR) {
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                OCX_GEN_STORE(ring[64 * i + lane] * scl[i * kRP + rl], zp + i * kRP * 128);
+                        } else {
+                            for (int i = 0; i * kRP < nrows; ++i)
+                                if (i * kRP + rl < nrows)
+                                    OCX_GEN_STORE(ring[64 * i + lane] * scl[i * kRP + rl], zp + i * kRP * 128);
+                        }
                     }
-                    const unsigned used = (unsigned)(nrows * 64);
+                    const unsigned used = (unsigned)(nrows * DF);
                     ring[lane] = ring[used + lane];  // the next rows' first normals to the front
                     head -= used;
                     t += nrows;
@@ -1369,6 +1423,7 @@ int ring_doubles(int64_t d, int DF, bool LR = false) {
     // (kPendMax 16-B entries) and one flag byte per ring slot
     if (DF == 64)
         return kRows64 * 64 + 64 + 8 + ((OCX_GEN_DEFER && !LR) ? 2 * kPendMax + (kRows64 * 64 + 64) / 8 : 0);
+    if (DF == 16 || DF == 32) return 512 + 64 + 512 / DF;  // a 512-normal batch + one round, the scales
     // a full batch of rows plus one round of normals
     int rb = 128;
     while (rb < (int64_t)batch_rows((int)d) * d + 65) rb *= 2;
@@ -1564,12 +1619,31 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
         int64_t wps4 = 0, wps6 = 0;
         const int64_t l4 = load(4, wps4), l6 = load(6, wps6);
         bool lr = l6 < l4 || (wps6 > wps4 && (double)l6 <= 1.06 * (double)l4);
+        // OCX_GEN_FORM=default|lr forces the form (tests, tuning and counter probes: the
+        // few-stream form's four-wave blocks place one wave per SIMD per 1 024 streams)
+        if (const char* ev = std::getenv("OCX_GEN_FORM")) {
+            if (!std::strcmp(ev, "lr")) lr = true;
+            else if (!std::strcmp(ev, "default")) lr = false;
+        }
         if (MODE == 0 && lr)
             return launch_wave_df<MODE, 64, true>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G,
                                                   zt, ytl, st_in, st_out, lab_in, lab_out, st,
                                                   t_off, nrows, labels);
         return launch_wave_df<MODE, 64>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
                                         st_in, st_out, lab_in, lab_out, st, t_off, nrows, labels);
+    }
+    // d = 16 / 32 rows that fill their lanes (P·C = d): the d = 64 loop's form over 512-normal
+    // batches (OCX_GEN_SMALL=0: the generic loop, tuning)
+    if constexpr (MODE == 0) {
+        const char* gs = std::getenv("OCX_GEN_SMALL");
+        if ((d == 16 || d == 32) && (int64_t)P * C == d && (!gs || std::atoi(gs) != 0)) {
+            if (d == 16)
+                return launch_wave_df<MODE, 16>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt,
+                                                ytl, st_in, st_out, lab_in, lab_out, st, t_off, nrows,
+                                                labels);
+            return launch_wave_df<MODE, 32>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt, ytl,
+                                            st_in, st_out, lab_in, lab_out, st, t_off, nrows, labels);
+        }
     }
     if (MODE == 0 && d == 1024 && (int64_t)P * C == 1024 && P <= 64)
         return launch_wave_df<MODE, 1024>(base_seed, T_seed, run0, B, nseq, T, d, P, C, G, zt,
@@ -1580,6 +1654,31 @@ hipError_t launch_wave(uint64_t base_seed, int64_t T_seed, int64_t run0, int64_t
 }
 
 }  // namespace
+
+namespace {
+template <int DF>
+int64_t resident_waves_df(int64_t d, int dev) {
+    constexpr int kBlock = gen_block(DF, false);
+    const size_t lds = (size_t)(ring_doubles(d, DF) + (DF == 0 && d > 128 ? kStackDoubles : 0)) * 8 *
+                       (kBlock / 64);
+    int q = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, DF>, kBlock, lds) !=
+            hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+    return (int64_t)q * (kBlock / 64) * cus;
+}
+}  // namespace
+
+// Streams the g(T) generator runs at once (one wave each) for rows of d on device `dev`: the
+// batch size below which it runs a single round (gT_run's batch sizing).
+int64_t ocx_gen_resident_waves(int64_t d, int dev) {
+    if (d == 1024) return resident_waves_df<1024>(d, dev);
+    if (d == 16) return resident_waves_df<16>(d, dev);
+    if (d == 32) return resident_waves_df<32>(d, dev);
+    if (d == 64) return resident_waves_df<64>(d, dev);
+    return resident_waves_df<0>(d, dev);
+}
 
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st) {

@@ -110,6 +110,7 @@ hipError_t ocx_launch_prefix_actions(const ocx_layout* L, const double* zt, cons
 hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y, double* zt,
                            double* ytl, hipStream_t st);
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
+int64_t ocx_gen_resident_waves(int64_t d, int dev);  // streams the generator runs in one round
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st);
 // the g(T) sampler's normals unclipped (the float32 twin clips them itself)

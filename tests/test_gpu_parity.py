@@ -149,7 +149,9 @@ def test_published_gT_curve(ocx):
 @pytest.mark.parametrize("B,T,d,P", [(70, 50, 5, 1), (33, 20, 64, 4), (5, 8, 1024, 64),
                                      (40, 9, 129, 0), (3, 11, 2, 0), (9, 6, 64, -1),
                                      (17, 7, 100, -2), (192, 2000, 64, 1), (6, 40, 1024, 1),
-                                     (4, 10, 1024, 0), (3, 5, 1024, -16), (70, 3, 1024, -32)])
+                                     (4, 10, 1024, 0), (3, 5, 1024, -16), (70, 3, 1024, -32),
+                                     (130, 301, 16, 8), (37, 700, 16, 1), (50, 123, 32, 8),
+                                     (9, 77, 32, -4), (21, 50, 16, -2)])
 def test_device_generator_matches_numpy(ocx, B, T, d, P):
     import torch
     eng = ocx["engine"]
@@ -175,6 +177,7 @@ def test_generator_forms_agree(ocx, monkeypatch, B, T):
     import torch
     eng = ocx["engine"]
     out = {}
+    monkeypatch.setenv("OCX_GEN_ROUNDS", "0")  # one launch of the form (not the rounds path)
     for form in ("default", "lr"):
         monkeypatch.setenv("OCX_GEN_FORM", form)
         db = eng.DeviceBatch(B, T, 64, lanes_per_seq=1).generate_gT(base_seed=3, run0=1)

@@ -25,6 +25,10 @@
 #   trail        tools/trail_probe.py (trailing pipeline vs sequential: configs[4], configs[3] T=1e5)
 #   trailtrace   rocprofv3 --kernel-trace of the trailing pipeline on the T = 1e5 case
 #   trailtraffic FETCH_SIZE / WRITE_SIZE of the trailing pipeline's kernels (tools/trail_traffic.py)
+#   genwaves     tools/genwaves_probe.py (generator time and SQ counters vs waves per SIMD, d = 1024
+#                and d = 64 forms), three PMC passes summed per launch size
+#   config4      tools/config4_probe.py (configs[4]: gen / FTRL per batch size, batches of whole waves)
+#   gpusub       a subset of pytest -m gpu (GPUSUB='-k expr' or file names)
 #   genscale     tools/genscale_probe.py (d = 1024 generator time vs streams per SIMD)
 #   cumask       tools/cumask_map (CU-mask placement) and tools/cumask_probe.py (CU-split overlap)
 #   config3      tools/perf_extra.py config3 (configs[2]: FTRL vs exact FTL, generation included)
@@ -116,6 +120,26 @@ for step in "$@"; do
     done
     python tools/trail_traffic.py "${O}_tpmc_FETCH_SIZE" "${O}_tpmc_WRITE_SIZE" 9800 100000 > "${O}_trailtraffic.json" || fail trailtraffic $?
     cat "${O}_trailtraffic.json" ;;
+  genwaves)
+    timeout -k 10 300 python -u tools/genwaves_probe.py > "${O}_genwaves.jsonl" 2> "${O}_genwaves.err" || fail genwaves $?
+    cat "${O}_genwaves.jsonl"
+    i=0
+    for CS in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+              "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_MISC" \
+              "SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_TRANS_F64 SQ_INST_CYCLES_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_FMA_F64"; do
+      i=$((i + 1))
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 240 rocprofv3 --pmc $CS --output-format csv -d "${O}_gwpmc$i" -o pmc -- python3 "$R/tools/genwaves_probe.py" --reps 1 > "${O}_gwpmc$i.log" 2>&1) || fail "genwaves pmc $i" $?
+    done
+    python tools/pmc_summary.py "${O}_gwpmc1" "${O}_gwpmc2" "${O}_gwpmc3" --kernel ocx_gen_wave --by-grid > "${O}_genwaves_pmc.txt"
+    cat "${O}_genwaves_pmc.txt" ;;
+  config4)
+    timeout -k 10 400 python -u tools/config4_probe.py > "${O}_config4.jsonl" 2> "${O}_config4.err" || fail config4 $?
+    cat "${O}_config4.jsonl" ;;
+  gpusub)
+    # a subset of the GPU suite: GPUSUB="-k expr" (or test files) chosen per call
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${GPUSUB:-} > "${O}_gpusub.log" 2>&1
+    rc=$?; tail -3 "${O}_gpusub.log"
+    [ $rc -eq 0 ] || fail gpusub $rc ;;
   genscale)
     timeout -k 10 300 python -u tools/genscale_probe.py > "${O}_genscale.jsonl" 2> "${O}_genscale.err" || fail genscale $?
     cat "${O}_genscale.jsonl" ;;

@@ -27,6 +27,29 @@ def main():
                               "seconds": dt, "timesteps_per_s": runs * T / dt,
                               "max_rel_vs_best": float(np.max(np.abs(reg - ref) / np.maximum(1, np.abs(ref))))}),
                   flush=True)
+    # generation and the FTRL pass apart, on the resident batch in the layout gT_regrets takes
+    # (OCX_LANES_BEST: lanes of two coordinates, up to 8)
+    import torch
+    for d in (8, 16, 32):
+        lanes = 8 if d >= 16 else 4
+        X = engine.DeviceBatch(runs, T, d, lanes_per_seq=lanes)
+        tg = tf = 1e9
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            X.generate_gT(0, 0)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            X.simulate_alg(closed_comparator=True)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            tg, tf = min(tg, t1 - t0), min(tf, t2 - t1)
+        print(json.dumps({"what": "split", "d": d, "T": T, "runs": runs, "lanes": lanes,
+                          "P": int(X.L.P), "C": int(X.L.C), "gen_ms": tg * 1e3, "ftrl_ms": tf * 1e3,
+                          "normals_per_s": runs * T * d / tg,
+                          "ftrl_frac_8tbs": runs * T * (8 * d + 8) / tf / 8e12}), flush=True)
+        del X
+        engine.release_buffers()
 
 
 if __name__ == "__main__":

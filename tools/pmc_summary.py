@@ -13,6 +13,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="")
+    ap.add_argument("--by-grid", action="store_true",
+                    help="one group per (kernel, grid size): launches of one kernel at several sizes")
     a = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
@@ -23,6 +25,8 @@ def main():
                 if a.kernel not in k:
                     continue
                 k = k[:70]
+                if a.by_grid:
+                    k = f"{k} grid={r.get('Grid_Size', '?')}"
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add((f, r["Dispatch_Id"]))
     for k, v in agg.items():
