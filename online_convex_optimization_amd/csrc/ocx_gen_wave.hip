@@ -1106,9 +1106,13 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             uint64_t* pend = reinterpret_cast<uint64_t*>(ring + RR * DF + 64 + 8);
             unsigned char* gone = reinterpret_cast<unsigned char*>(ring + RR * DF + 64 + 8 + 2 * kPendMax);
             int npend = 0;
-            while (produced < total) {
+            // (head > 0 once everything is drawn: at DF < 64 the <= 63 normals left over from a
+            // batch can hold the last rows whole)
+            while (produced < total || head > 0) {
 #if OCX_GEN_INNER
-                if (total - produced >= (uint32_t)(RR * DF + 64)) {
+                if (produced == total) {
+                    // only the rows left in the ring to write
+                } else if (total - produced >= (uint32_t)(RR * DF + 64)) {
                     // a whole batch still to draw: full rounds until the ring holds it, with
                     // one loop test per round (no per-round need / last-round / batch tests;
                     // every round here has 64 or more normals left to draw — with deferred
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
                     if constexpr (kDF) resolve_wedges(ring, pend, gone, npend, head, produced, tb, lane);
                 } else
 #endif
-                {
+                if (produced < total) {
                     const uint32_t left = total - produced;
                     const int n =
                         left >= 64u ? zig_round<true, true, true>(w, 64, tb, ring, 0, head, lane)
@@ -1500,7 +1504,7 @@ struct OvGeom {
     size_t lds = 0;
     int per_cu = 0;
 };
-template <int OV>
+template <int DF, int OV>
 OvGeom ov_geometry(int dev, int wps) {
     static std::mutex mu;
     static std::map<std::pair<int, int>, OvGeom> cache;
@@ -1513,11 +1517,11 @@ OvGeom ov_geometry(int dev, int wps) {
     if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) !=
             hipSuccess || lds_cu <= 0)
         lds_cu = 160 * 1024;
-    const size_t base = (size_t)ring_doubles(64, 64) * 8 * 4;  // four waves' rings
+    const size_t base = (size_t)ring_doubles(DF, DF) * 8 * 4;  // four waves' rings
     size_t lds = base;
     int q = 0;
     for (; lds <= (size_t)lds_cu; lds += 512) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, 64, false, false, OV>,
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&q, ocx_gen_wave_kernel<0, DF, false, false, OV>,
                                                          256, lds) != hipSuccess)
             break;
         if (q <= wps) break;
@@ -1530,12 +1534,10 @@ OvGeom ov_geometry(int dev, int wps) {
 
 }  // namespace
 
-hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
-                                   int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
-                                   hipStream_t st) {
-    if (nseq <= 0 || L->T == 0) return hipSuccess;
-    if (L->d != 64 || L->P * L->C != 64 || b_off % 4 || nseq % 4) return hipErrorInvalidValue;
-    if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+namespace {
+template <int DF>
+hipError_t launch_gen_range_df(const ocx_layout* L, uint64_t base_seed, int64_t run0, int64_t b_off,
+                               int64_t nseq, int wps, double* zt, double* ytl, hipStream_t st) {
     int dev = 0, cus = 256;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -1544,24 +1546,40 @@ hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int6
     // up to three waves per SIMD the 128-VGPR form (one FTRL wave of <= 128 VGPRs fits
     // beside it); four or more: the 96-VGPR form (a few spills)
     const bool w4 = wps >= 4;
-    const OvGeom gm = w4 ? ov_geometry<5>(dev, wps) : ov_geometry<4>(dev, wps);
+    const OvGeom gm = w4 ? ov_geometry<DF, 5>(dev, wps) : ov_geometry<DF, 4>(dev, wps);
     const int64_t resident = (int64_t)cus * 4 * std::max(1, std::min(gm.per_cu, wps));
     const int64_t per_wave = (nseq + resident - 1) / resident;
     const unsigned blocks = (unsigned)(((nseq + per_wave - 1) / per_wave + 3) / 4);
     const int64_t nwaves = (int64_t)blocks * 4;
     if (w4)
-        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, 5>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, DF, false, false, 5>), dim3(blocks), dim3(256),
                            gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
                            (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
                            (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                           ring_doubles(64, 64), nwaves, b_off, (int64_t)0, L->T, 1);
+                           ring_doubles(DF, DF), nwaves, b_off, (int64_t)0, L->T, 1);
     else
-        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, 64, false, false, 4>), dim3(blocks), dim3(256),
+        hipLaunchKernelGGL((ocx_gen_wave_kernel<0, DF, false, false, 4>), dim3(blocks), dim3(256),
                            gm.lds, st, base_seed, L->T, run0, L->B, nseq, L->T, (int)L->d,
                            (int)L->P, (int)L->C, L->G, zt, ytl, (const uint64_t*)nullptr,
                            (uint64_t*)nullptr, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                           ring_doubles(64, 64), nwaves, b_off, (int64_t)0, L->T, 1);
+                           ring_doubles(DF, DF), nwaves, b_off, (int64_t)0, L->T, 1);
     return hipGetLastError();
+}
+}  // namespace
+
+// The overlapped pipeline's generator: rows of d = 16 / 32 / 64 filling their lanes (P·C = d), in
+// four-wave blocks over sequences [b_off, b_off + nseq) of L, at most `wps` waves per SIMD (see
+// ov_geometry).
+hipError_t ocx_launch_gen_gT_range(const ocx_layout* L, uint64_t base_seed, int64_t run0,
+                                   int64_t b_off, int64_t nseq, int wps, double* zt, double* ytl,
+                                   hipStream_t st) {
+    if (nseq <= 0 || L->T == 0) return hipSuccess;
+    if ((L->d != 64 && L->d != 32 && L->d != 16) || L->P * L->C != L->d || b_off % 4 || nseq % 4)
+        return hipErrorInvalidValue;
+    if (L->T * L->d >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    if (L->d == 16) return launch_gen_range_df<16>(L, base_seed, run0, b_off, nseq, wps, zt, ytl, st);
+    if (L->d == 32) return launch_gen_range_df<32>(L, base_seed, run0, b_off, nseq, wps, zt, ytl, st);
+    return launch_gen_range_df<64>(L, base_seed, run0, b_off, nseq, wps, zt, ytl, st);
 }
 
 // The few-stream (LR) form over sequences [b_off, b_off + nseq) of L, one wave per stream,
@@ -1688,8 +1706,8 @@ hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t ru
     // (ocx_run_gen_rounds), bit-identical; OCX_GEN_ROUNDS=0 keeps the single launch (tuning),
     // and so does a stream whose capture cannot fork (ocx_stream_fork_ok)
     const char* gr = std::getenv("OCX_GEN_ROUNDS");
-    if ((!gr || std::atoi(gr) != 0) && ocx_pipeline_supported(L) && ocx_pipeline_worth(L, 4) &&
-        ocx_stream_fork_ok(st))
+    if ((!gr || std::atoi(gr) != 0) && L->d == 64 && ocx_pipeline_supported(L) &&
+        ocx_pipeline_worth(L, 4) && ocx_stream_fork_ok(st))
         return ocx_run_gen_rounds(L, base_seed, run0, zt, ytl, st);
     return launch_wave<0>(base_seed, L->T, run0, L->B, nseq, L->T, L->d, L->P, L->C, L->G, zt,
                           ytl, nullptr, nullptr, nullptr, nullptr, st);

@@ -107,9 +107,14 @@ bool ocx_stream_fork_ok(hipStream_t st) {
     return hipRuntimeGetVersion(&v) == hipSuccess && v >= 70200000;
 }
 
+// The layouts the sub-batch pipeline runs: d = 64 in the lean pipelined FTRL form's layouts
+// (8 x 8, 16 x 4), and (round 6) the g(T) layouts of d = 16 / 32 (butterfly lanes of 2 / 4
+// coordinates, P·C = d), whose FTRL side is the plain kernel over a group range
+// (ocx_launch_alg_range).
 bool ocx_pipeline_supported(const ocx_layout* L) {
-    return L->d == 64 && L->P * L->C == 64 && ocx_pipe_lean_supported(L) && L->T > 0 &&
-           L->T * L->d < ((int64_t)1 << 32);
+    if (L->T <= 0 || L->T * L->d >= ((int64_t)1 << 32) || L->P * L->C != L->d) return false;
+    if (L->d == 64) return ocx_pipe_lean_supported(L);
+    return (L->d == 16 || L->d == 32) && !L->chain && L->P == 8 && (L->C == 2 || L->C == 4);
 }
 
 // Whether cutting L's batch into generator rounds of `wps` waves per SIMD pays: at least four
@@ -139,7 +144,7 @@ hipError_t ocx_run_gen_rounds(const ocx_layout* L, uint64_t base_seed, int64_t r
     const char* fe = std::getenv("OCX_GEN_ROUNDS_FORM");
     const bool lr6 = !fe || std::strcmp(fe, "lr6") == 0;
     const int wps = (fe && std::strcmp(fe, "ov5") == 0) ? 5 : (lr6 ? 6 : 4);
-    if (!ocx_pipeline_supported(L)) return hipErrorInvalidValue;
+    if (!ocx_pipeline_supported(L) || L->d != 64) return hipErrorInvalidValue;
     int dev = 0, cus = 256;
     OCX_PIPE_TRY(hipGetDevice(&dev));
     OCX_PIPE_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -237,8 +242,10 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], gs));
             OCX_PIPE_TRY(hipStreamWaitEvent(ss, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
-                OCX_PIPE_TRY(ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S, nb / S,
-                                                      gmax, ss));
+                OCX_PIPE_TRY(L->d == 64 ? ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass,
+                                                                   b0 / S, nb / S, gmax, ss)
+                                        : ocx_launch_alg_range(L, zt, yt, eta0, regret, onepass,
+                                                               b0 / S, nb / S, gmax, ss));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], ss));
             c.sim_recorded[(size_t)i] = 1;
         }
@@ -327,11 +334,26 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
     PipeCtx& c = g_pipe[dev];
     std::lock_guard<std::mutex> lk(c.mu);
     OCX_PIPE_TRY(pipe_init(c));
-    // chunks of whole 64-step blocks (the FTRL state's refresh points), at least two
+    // chunks of whole 64-step blocks (the FTRL state's refresh points), at least two.  Each
+    // batch's FTRL pass can start only once the generator has drawn the batch's labels (after
+    // all its normals), and the next batch's first generator chunk only once that pass has read
+    // chunk 0: with equal chunks the generator idled for one FTRL chunk per batch (≈5 ms of a
+    // ≈120 ms period at T = 1e5, profiles/r05_trail_kernel_trace.csv).  So the horizon starts
+    // with a ramp (round 6): chunks of `ramp` blocks, doubling up to the standard size — the
+    // reader, ≈2.3× faster per row than the writer, stays a chunk ahead from the first one.
+    // OCX_TRAIL_RAMP (blocks, default 4; 0 = equal chunks) is a tuning knob.
     const int64_t blocks = (L->T + 63) / 64;
     const int64_t n = std::max<int64_t>(2, std::min<int64_t>(nchunks, blocks));
-    const int64_t tc = (blocks + n - 1) / n * 64;
-    const int64_t nch = (L->T + tc - 1) / tc;
+    const int64_t std_blocks = (blocks + n - 1) / n;
+    int64_t ramp = 4;
+    if (const char* e = std::getenv("OCX_TRAIL_RAMP")) ramp = std::max<int64_t>(0, std::atoll(e));
+    std::vector<int64_t> cstart;  // first step of each chunk; cstart.back() == T
+    for (int64_t b = 0, r = ramp > 0 ? ramp : std_blocks; b < blocks; r *= 2) {
+        cstart.push_back(b * 64);
+        b += std::min(std::min(r, std_blocks), blocks - b);
+    }
+    cstart.push_back(L->T);
+    const int64_t nch = (int64_t)cstart.size() - 1;
     OCX_PIPE_TRY(ensure_events(c, (size_t)nch));
     const int64_t words = L->G * L->S * 6;
     double* yts[2] = {yt0, yt1};
@@ -348,7 +370,7 @@ hipError_t ocx_run_gen_sim_trailing(const ocx_layout* L, uint64_t base_seed, int
         const bool next = k + 1 < nbatch;
         const int64_t rk = run0 + (k + 1) * L->B;
         for (int64_t ci = 0; ci < nch; ++ci) {
-            const int64_t t0 = ci * tc, tn = std::min(tc, L->T - t0);
+            const int64_t t0 = cstart[(size_t)ci], tn = cstart[(size_t)ci + 1] - t0;
             OCX_PIPE_TRY(ocx_launch_alg_pipe_chunk(lay(k), zt, yk, eta0, regret + k * L->B, 1, t0, tn,
                                                    fst, bad + k, gmax, F));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)ci], F));

@@ -40,18 +40,23 @@
 #ifndef OCX_ALG_MIN_WAVES
 #define OCX_ALG_MIN_WAVES 1
 #endif
-template <int C, int P, bool CHAIN, int NB>
-__global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void ocx_alg_kernel(
+// MINW > 0: the register budget of MINW waves per SIMD (the small-d pipeline's FTRL side asks for
+// 4: <= 128 VGPRs, one wave beside four 96-VGPR generator waves)
+template <int C, int P, bool CHAIN, int NB, int MINW = 0>
+__global__ __launch_bounds__(OCX_BLOCK, (MINW > 0 ? MINW : (C <= 16 ? OCX_ALG_MIN_WAVES : 1))) void ocx_alg_kernel(
     const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T,
     int64_t d, int64_t G, int algo, double eta0, const double* __restrict__ comparator,
     double* __restrict__ regret, double* __restrict__ cum_out, double* __restrict__ comp_out,
     double* __restrict__ x_last, double* __restrict__ cmp_out, int* __restrict__ regime_out,
-    int onepass, int norm) {
+    int onepass, int norm, int64_t g0, int64_t gn, unsigned long long* __restrict__ gmax) {
     constexpr int S = 64 / P;
     constexpr int K = C / 2;
     const int lane = threadIdx.x & 63;
-    const int64_t g = ocx_wave_id();
-    if (g >= G) return;
+    // wave-groups [g0, g0 + gn) of the layout (a sub-batch of the overlapped pipeline; the
+    // whole layout otherwise), G the layout's groups (the plane stride)
+    const int64_t wv = ocx_wave_id();
+    if (wv >= gn) return;
+    const int64_t g = g0 + wv;
 #ifdef OCX_ALG_PRIO  // tuning: issue priority over waves of a kernel running beside it
     __builtin_amdgcn_s_setprio(OCX_ALG_PRIO);
 #endif
@@ -197,6 +202,20 @@ __global__ __launch_bounds__(OCX_BLOCK, (C <= 16 ? OCX_ALG_MIN_WAVES : 1)) void 
         if (closed) comp = 0.5 * (double)T - nrm;
     }
 
+    // g(T) folded in (the small-d pipeline's FTRL launches; ocx_alg_pipe.hip does the same): a
+    // max over the wave's sequences, one 64-bit atomic max of the bit pattern per wave —
+    // positive doubles order as their bits and a NaN never passes `>`, so this selects what
+    // ocx_max_fold_kernel and the host's loop select
+    if (gmax != nullptr && __ballot(b < B) != 0) {  // wave-uniform
+        const double rg = cum - comp;
+        double mv = (c == 0 && b < B && rg > 0.0) ? rg : 0.0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double u = __shfl_xor(mv, o, 64);
+            if (u > mv) mv = u;
+        }
+        if (lane == 0 && mv > 0.0) atomicMax(gmax, (unsigned long long)__double_as_longlong(mv));
+    }
     if (c == 0 && b < B) {
         if (regret) regret[b] = cum - comp;
         if (cum_out) cum_out[b] = cum;
@@ -466,8 +485,26 @@ hipError_t launch_alg_cp(const ocx_layout* L, const double* zt, const double* yt
                          hipStream_t st) {
     hipLaunchKernelGGL((ocx_alg_kernel<C, P, CH, nb_for(C, P)>), OCX_SHAPE(L->G), 0, st, zt, yt,
                        L->B, L->T, L->d, L->G, algo, eta0, cmp, reg, cum, comp, xl, cmp_out,
-                       regime, onepass, norm);
+                       regime, onepass, norm, (int64_t)0, L->G, (unsigned long long*)nullptr);
     return hipGetLastError();
+}
+
+// FTRL over wave-groups [g0, g0 + gn) of L with g(T) folded into gmax (nullable): the small-d
+// pipeline's FTRL side (ocx_pipeline.hip), the g(T) layouts of 16 <= d < 64 (butterfly, 8 lanes)
+template <int C, int P, bool CH>
+hipError_t launch_alg_range_cp(const ocx_layout* L, const double* zt, const double* yt,
+                               double eta0, double* reg, int onepass, int64_t g0, int64_t gn,
+                               unsigned long long* gmax, hipStream_t st) {
+    if constexpr (CH) {
+        return hipErrorInvalidValue;
+    } else {
+        // one-wave blocks: the dispatcher spreads them over the SIMDs the generator leaves room on
+        hipLaunchKernelGGL((ocx_alg_kernel<C, P, false, nb_for(C, P), 4>), ocx_grid(gn, 1), dim3(64), 0,
+                           st, zt, yt, L->B, L->T, L->d, L->G, 0, eta0, (const double*)nullptr, reg,
+                           (double*)nullptr, (double*)nullptr, (double*)nullptr, (double*)nullptr,
+                           (int*)nullptr, onepass, 0, g0, gn, gmax);
+        return hipGetLastError();
+    }
 }
 
 template <int C, int P, bool CH>
@@ -518,6 +555,18 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
         return ocx_launch_alg_pipe(L, zt, yt, algo, eta0, reg, cum, comp, regime, onepass, st);
     OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
                  onepass, norm, st)
+}
+
+hipError_t ocx_launch_alg_range(const ocx_layout* L, const double* zt, const double* yt,
+                                double eta0, double* reg, int onepass, int64_t g0, int64_t gn,
+                                unsigned long long* gmax, hipStream_t st) {
+    if (gn <= 0) return hipSuccess;
+    if (g0 < 0 || g0 + gn > L->G || L->chain) return hipErrorInvalidValue;
+    // the g(T) layouts of 16 <= d < 64: 8 lanes of 2 or 4 coordinates
+    if (L->P != 8) return hipErrorInvalidValue;
+    if (L->C == 2) return launch_alg_range_cp<2, 8, false>(L, zt, yt, eta0, reg, onepass, g0, gn, gmax, st);
+    if (L->C == 4) return launch_alg_range_cp<4, 8, false>(L, zt, yt, eta0, reg, onepass, g0, gn, gmax, st);
+    return hipErrorInvalidValue;
 }
 
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,

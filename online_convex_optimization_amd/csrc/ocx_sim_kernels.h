@@ -111,6 +111,11 @@ hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y
                            double* ytl, hipStream_t st);
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
 int64_t ocx_gen_resident_waves(int64_t d, int dev);  // streams the generator runs in one round
+// FTRL over wave-groups [g0, g0 + gn) of a tree layout with C in {2, 4} (the small-d pipeline's
+// FTRL side), g(T) folded into gmax (nullable)
+hipError_t ocx_launch_alg_range(const ocx_layout* L, const double* zt, const double* yt,
+                                double eta0, double* reg, int onepass, int64_t g0, int64_t gn,
+                                unsigned long long* gmax, hipStream_t st);
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st);
 // the g(T) sampler's normals unclipped (the float32 twin clips them itself)

@@ -151,7 +151,8 @@ def test_published_gT_curve(ocx):
                                      (17, 7, 100, -2), (192, 2000, 64, 1), (6, 40, 1024, 1),
                                      (4, 10, 1024, 0), (3, 5, 1024, -16), (70, 3, 1024, -32),
                                      (130, 301, 16, 8), (37, 700, 16, 1), (50, 123, 32, 8),
-                                     (9, 77, 32, -4), (21, 50, 16, -2)])
+                                     (9, 77, 32, -4), (21, 50, 16, -2), (37, 257, 16, 8),
+                                     (19, 33, 32, 8), (11, 65, 16, 8)])
 def test_device_generator_matches_numpy(ocx, B, T, d, P):
     import torch
     eng = ocx["engine"]

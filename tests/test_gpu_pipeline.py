@@ -23,11 +23,15 @@ def eng():
     return engine
 
 
-@pytest.mark.parametrize("B,T,lanes,sub", [(3000, 300, 8, 512), (2048, 257, 16, 0),
-                                           (1000, 64, 128, 0), (36000, 40, 128, 0)])
-def test_pipelined_equals_sequential(eng, B, T, lanes, sub):
+@pytest.mark.parametrize("B,T,d,lanes,sub", [(3000, 300, 64, 8, 512), (2048, 257, 64, 16, 0),
+                                             (1000, 64, 64, 128, 0), (36000, 40, 64, 128, 0),
+                                             (3000, 300, 16, 8, 512), (20000, 77, 16, 8, 0),
+                                             (2500, 129, 32, 8, 1024), (17000, 50, 32, 8, 0)])
+def test_pipelined_equals_sequential(eng, B, T, d, lanes, sub):
+    """d = 64 in the lean pipelined FTRL layouts; d = 16 / 32 (round 6) in the g(T) layouts of
+    8 lanes (2 / 4 coordinates each), whose FTRL side is the plain kernel over group ranges."""
     import torch
-    d, nb = 64, 3
+    nb = 3
     db = eng.DeviceBatch(B, T, d, lanes_per_seq=lanes)
     out = {}
     for mode in (False, True):
@@ -46,6 +50,23 @@ def test_pipelined_equals_sequential(eng, B, T, lanes, sub):
     for b in (0, B - 1):
         z, y = O.gT_sample(9, T, 5 + 2 * B + b, d)
         assert close_closed(out[True][0][b], O.simulate_alg(z, y, 0, SQ2), T), b
+
+
+@pytest.mark.parametrize("T,d,runs", [(120, 16, 40000), (60, 32, 33000)])
+def test_gT_small_d_pipeline_equals_sequential(eng, monkeypatch, T, d, runs):
+    """engine.gT_regrets / gT_max at d = 16 / 32 (configs[1]'s g(T) layouts) through the sub-batch
+    pipeline (round 6) equal the sequential loop (OCX_PIPELINE=0) bit for bit, and sampled
+    sequences are within the closed-form bar of the oracle."""
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("OCX_PIPELINE", pipe)
+        out[pipe] = (eng.gT_regrets(T, runs, base_seed=12, d=d, run0=3),
+                     eng.gT_max(T, runs, base_seed=12, d=d, run0=3))
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1] == eng.max_regret(out["0"][0])
+    for r in (0, runs // 3, runs - 1):
+        z, y = O.gT_sample(12, T, 3 + r, d)
+        assert close_closed(out["1"][0][r], O.simulate_alg(z, y, 0, SQ2), T), r
 
 
 def test_pipelined_exact_layout_two_pass(eng):

@@ -1,9 +1,10 @@
 """configs[4] (d = 1024, T = 1e4): where a batch's time goes and how the batch size sets it.
 
-Prints the free HBM, then per resident batch size B the generator and the FTRL pass apart
-(DeviceBatch, OCX_LANES_BEST = 32 x 32), then engine.gT_regrets over `runs` runs with batches
-of whole generator waves per SIMD (the default since round 6) and with equal batches
-(OCX_BATCH_WAVES=0).  One JSON line each.
+Prints the free HBM, then engine.gT_regrets over `runs` runs with batches of whole generator
+waves per SIMD (the default since round 6) and with equal batches (OCX_BATCH_WAVES=0), then per
+resident batch size B the generator and the FTRL pass apart (DeviceBatch, OCX_LANES_BEST =
+32 x 32).  One JSON line each.  (The engine sizes its batches by the free HBM: the g(T) calls
+come first, before any DeviceBatch has grown torch's cache.)
 
     python tools/config4_probe.py [--runs 32768] [--sizes 2048,2731,2979,3072]
 """
@@ -28,6 +29,25 @@ def main():
     T, d = a.T, 1024
     free, total = torch.cuda.mem_get_info()
     print(json.dumps({"what": "hbm", "free_GiB": free / 2**30, "total_GiB": total / 2**30}), flush=True)
+    engine.release_buffers()
+    ref = None
+    for bw in ("1", "0"):
+        os.environ["OCX_BATCH_WAVES"] = bw
+        engine.gT_regrets(T, 2048, d=d)  # warm
+        t0 = time.perf_counter()
+        reg = engine.gT_regrets(T, a.runs, d=d)
+        dt = time.perf_counter() - t0
+        if ref is None:
+            ref = reg
+        import numpy as np
+        print(json.dumps({"what": "config4_gT", "T": T, "runs": a.runs, "d": d,
+                          "batch_waves": bw == "1", "seconds": dt,
+                          "free_GiB_after": torch.cuda.mem_get_info()[0] / 2**30,
+                          "timesteps_per_s": T * a.runs / dt,
+                          "same_regrets": bool(np.array_equal(reg, ref)),
+                          "g": engine.max_regret(reg)}), flush=True)
+        engine.release_buffers()
+    os.environ.pop("OCX_BATCH_WAVES", None)
     for B in (int(x) for x in a.sizes.split(",") if x):
         try:
             X = engine.DeviceBatch(B, T, d)
@@ -51,25 +71,9 @@ def main():
                           "ftrl_TBps": B * T * (8 * d + 8) / tf / 1e12,
                           "ns_per_stream_step": (tg + tf) / (B * T) * 1e9}), flush=True)
         del X
+        import gc
+        gc.collect()
         torch.cuda.empty_cache()
-    engine.release_buffers()
-    ref = None
-    for bw in ("1", "0"):
-        os.environ["OCX_BATCH_WAVES"] = bw
-        engine.gT_regrets(T, 2048, d=d)  # warm
-        t0 = time.perf_counter()
-        reg = engine.gT_regrets(T, a.runs, d=d)
-        dt = time.perf_counter() - t0
-        if ref is None:
-            ref = reg
-        import numpy as np
-        print(json.dumps({"what": "config4_gT", "T": T, "runs": a.runs, "d": d,
-                          "batch_waves": bw == "1", "seconds": dt,
-                          "timesteps_per_s": T * a.runs / dt,
-                          "same_regrets": bool(np.array_equal(reg, ref)),
-                          "g": engine.max_regret(reg)}), flush=True)
-        engine.release_buffers()
-    os.environ.pop("OCX_BATCH_WAVES", None)
 
 
 if __name__ == "__main__":

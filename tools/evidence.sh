@@ -108,7 +108,7 @@ for step in "$@"; do
     python tools/overlap_report.py "${O}_otrace" > "${O}_otrace.json" || fail overlap_report $?
     cut -c1-400 "${O}_otrace.json" ;;
   trail)
-    timeout -k 10 600 python -u tools/trail_probe.py --cases "${TRAIL_CASES:-c4,t1e5}" --chunks "${TRAIL_CHUNKS:-12}" > "${O}_trail.jsonl" 2> "${O}_trail.err" || fail trail $?
+    timeout -k 10 600 python -u tools/trail_probe.py --cases "${TRAIL_CASES:-c4,t1e5}" --chunks "${TRAIL_CHUNKS:-12}" --ramps "${TRAIL_RAMPS:-}" > "${O}_trail.jsonl" 2> "${O}_trail.err" || fail trail $?
     cut -c1-260 "${O}_trail.jsonl" ;;
   trailtrace)
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace -d "${O}_ttrace" -o tt --output-format csv -- python3 "$R/tools/trail_probe.py" --cases t1e5 --runs-t5 19600 --check 0 > "${O}_ttrace.log" 2>&1) || fail trailtrace $?
@@ -137,7 +137,7 @@ for step in "$@"; do
     cat "${O}_config4.jsonl" ;;
   gpusub)
     # a subset of the GPU suite: GPUSUB="-k expr" (or test files) chosen per call
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${GPUSUB:-} > "${O}_gpusub.log" 2>&1
+    timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread ${GPUSUB:-tests} > "${O}_gpusub.log" 2>&1
     rc=$?; tail -3 "${O}_gpusub.log"
     [ $rc -eq 0 ] || fail gpusub $rc ;;
   genscale)
