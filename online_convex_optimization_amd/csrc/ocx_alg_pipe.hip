@@ -463,10 +463,18 @@ bool ocx_pipe_lean_supported(const ocx_layout* L) {
     return !L->chain && L->T < ((int64_t)1 << 30) && ((L->P == 8 && L->C == 8) || (L->P == 16 && L->C == 4));
 }
 
+// The layouts the lean form is built for beyond the trailing pipeline's: 8 x 4 (d = 32's
+// g(T) layout in the sub-batch pipeline, round 6).
+bool ocx_pipe_lean_launchable(const ocx_layout* L) {
+    return ocx_pipe_lean_supported(L) || (!L->chain && L->T < ((int64_t)1 << 30) && L->P == 8 && L->C == 4);
+}
+
 namespace {
 hipError_t launch_lean(const ocx_layout* L, const PipeArgs& a, hipStream_t st) {
     const dim3 grid = ocx_grid(a.gn, 1), block(64);
-    if (L->P == 8 && L->C == 8) {
+    if (L->P == 8 && L->C == 4 && !a.state) {
+        hipLaunchKernelGGL((ocx_alg_pipe_kernel<4, 8, OCX_PIPE_LEAN_NB4, false, 4>), grid, block, 0, st, a);
+    } else if (L->P == 8 && L->C == 8) {
         if (a.state)
             hipLaunchKernelGGL((ocx_alg_pipe_kernel<8, 8, OCX_PIPE_LEAN_NB8, false, 4, true>), grid, block, 0, st, a);
         else

@@ -114,7 +114,11 @@ bool ocx_stream_fork_ok(hipStream_t st) {
 bool ocx_pipeline_supported(const ocx_layout* L) {
     if (L->T <= 0 || L->T * L->d >= ((int64_t)1 << 32) || L->P * L->C != L->d) return false;
     if (L->d == 64) return ocx_pipe_lean_supported(L);
-    return (L->d == 16 || L->d == 32) && !L->chain && L->P == 8 && (L->C == 2 || L->C == 4);
+    // the FTRL side must be the arithmetic the sequential loop runs (ocx_launch_alg): the
+    // pipelined kernel's lean form where that loop takes the pipelined kernel (8 x 4), the
+    // plain kernel over group ranges otherwise (8 x 2)
+    return (L->d == 16 || L->d == 32) && !L->chain && L->P == 8 &&
+           (ocx_pipe_supported(L) ? ocx_pipe_lean_launchable(L) : L->C == 2);
 }
 
 // Whether cutting L's batch into generator rounds of `wps` waves per SIMD pays: at least four
@@ -242,10 +246,11 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
             OCX_PIPE_TRY(hipEventRecord(c.ev_gen[(size_t)i], gs));
             OCX_PIPE_TRY(hipStreamWaitEvent(ss, c.ev_gen[(size_t)i], 0));
             if (!skip_sim)
-                OCX_PIPE_TRY(L->d == 64 ? ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass,
-                                                                   b0 / S, nb / S, gmax, ss)
-                                        : ocx_launch_alg_range(L, zt, yt, eta0, regret, onepass,
-                                                               b0 / S, nb / S, gmax, ss));
+                OCX_PIPE_TRY(ocx_pipe_supported(L)
+                                 ? ocx_launch_alg_pipe_lean(L, zt, yt, eta0, regret, onepass, b0 / S,
+                                                            nb / S, gmax, ss)
+                                 : ocx_launch_alg_range(L, zt, yt, eta0, regret, onepass, b0 / S,
+                                                        nb / S, gmax, ss));
             OCX_PIPE_TRY(hipEventRecord(c.ev_sim[(size_t)i], ss));
             c.sim_recorded[(size_t)i] = 1;
         }

@@ -562,10 +562,9 @@ hipError_t ocx_launch_alg_range(const ocx_layout* L, const double* zt, const dou
                                 unsigned long long* gmax, hipStream_t st) {
     if (gn <= 0) return hipSuccess;
     if (g0 < 0 || g0 + gn > L->G || L->chain) return hipErrorInvalidValue;
-    // the g(T) layouts of 16 <= d < 64: 8 lanes of 2 or 4 coordinates
-    if (L->P != 8) return hipErrorInvalidValue;
-    if (L->C == 2) return launch_alg_range_cp<2, 8, false>(L, zt, yt, eta0, reg, onepass, g0, gn, gmax, st);
-    if (L->C == 4) return launch_alg_range_cp<4, 8, false>(L, zt, yt, eta0, reg, onepass, g0, gn, gmax, st);
+    // d = 16's g(T) layout: 8 lanes of 2 coordinates (8 x 4 runs the pipelined kernel's lean form)
+    if (L->P == 8 && L->C == 2)
+        return launch_alg_range_cp<2, 8, false>(L, zt, yt, eta0, reg, onepass, g0, gn, gmax, st);
     return hipErrorInvalidValue;
 }
 

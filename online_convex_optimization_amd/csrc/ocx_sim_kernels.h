@@ -59,6 +59,7 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
                                      int wps, int64_t sub_seqs, hipStream_t st);
 // generation of batch k+1 trailing the chunked FTRL pass over batch k in one z buffer
 // (ocx_pipeline.hip: the capacity-limited batches); see there for the buffers
+bool ocx_pipe_lean_launchable(const ocx_layout* L);  // ocx_launch_alg_pipe_lean's layouts
 bool ocx_trailing_supported(const ocx_layout* L);
 // the largest batch whose generator waves all fit beside the FTRL chunks' waves
 int64_t ocx_trailing_max_batch(const ocx_layout* L);
@@ -111,8 +112,8 @@ hipError_t ocx_launch_pack(const ocx_layout* L, const double* z, const double* y
                            double* ytl, hipStream_t st);
 hipError_t ocx_launch_max(const double* r, int64_t B, double* out, hipStream_t st);
 int64_t ocx_gen_resident_waves(int64_t d, int dev);  // streams the generator runs in one round
-// FTRL over wave-groups [g0, g0 + gn) of a tree layout with C in {2, 4} (the small-d pipeline's
-// FTRL side), g(T) folded into gmax (nullable)
+// FTRL over wave-groups [g0, g0 + gn) of the 8 x 2 tree layout (the small-d pipeline's FTRL side
+// at d = 16), g(T) folded into gmax (nullable)
 hipError_t ocx_launch_alg_range(const ocx_layout* L, const double* zt, const double* yt,
                                 double eta0, double* reg, int onepass, int64_t g0, int64_t gn,
                                 unsigned long long* gmax, hipStream_t st);

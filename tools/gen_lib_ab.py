@@ -26,8 +26,10 @@ def lib(name):
 def main():
     st = torch.cuda.current_stream()
     libs = [(n, lib(n)) for n in sys.argv[1].split(",")]
-    for B, T, d in ((3000, 1000, 64), (32768, 10000, 64), (4900, 100000, 64),
-                    (2048, 10000, 1024)):
+    shapes = ((3000, 1000, 64), (32768, 10000, 64), (4900, 100000, 64), (2048, 10000, 1024))
+    if os.environ.get("GENAB_SHAPES"):  # "B:T:d,..."
+        shapes = tuple(tuple(int(v) for v in c.split(":")) for c in os.environ["GENAB_SHAPES"].split(","))
+    for B, T, d in shapes:
         db = engine.DeviceBatch(B, T, d, lanes_per_seq=engine.LANES_BEST)
         sums = []
         for n, L in libs:  # one buffer (the big shapes fill HBM): compare wrapping sums
