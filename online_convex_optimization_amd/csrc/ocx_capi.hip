@@ -1069,7 +1069,9 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             // 131 072 runs: 8 -> 4.06-4.08e9, 12 -> 4.13-4.17e9, 16 -> 4.06e9 timesteps/s; making
             // FTRL chunk c wait for the generator's chunk c - 2, 3 or 4 (so the reader does not
             // run ahead) measured no better (profiles/r05_trail_pace.jsonl, r05_trail_chunks.jsonl)
-            int nch = 12;
+            // round 6, with the ramp (ocx_run_gen_sim_trailing): 8 chunks 4.20e9, 12 4.16e9
+            // (profiles/r06_trail.jsonl)
+            int nch = 8;
             if (const char* e = std::getenv("OCX_TRAIL_CHUNKS")) nch = std::max(2, std::atoi(e));
             OCX_HIP(ocx_run_gen_sim_trailing(&Lp, base_seed, run0, nfull, cx->zt.as<double>(),
                                              cx->yt.as<double>(), cx->yt2.as<double>(),

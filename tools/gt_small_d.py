@@ -17,7 +17,7 @@ def main():
     for d in (5, 8, 16, 32):
         ref = None
         for name, lanes in (("best", engine.LANES_BEST), ("exact", 1)):
-            engine.gT_regrets(T, 4096, base_seed=0, d=d, lanes_per_seq=lanes)  # warm up
+            engine.gT_regrets(T, runs, base_seed=0, d=d, lanes_per_seq=lanes)  # warm: same shape
             t0 = time.perf_counter()
             reg = engine.gT_regrets(T, runs, base_seed=0, d=d, lanes_per_seq=lanes)
             dt = time.perf_counter() - t0
