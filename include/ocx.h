@@ -187,9 +187,10 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * for any rows and labels (no regime: where the closed forms above do not apply), on device
  * by a primal log-barrier path (damped Newton, μ from 1 to 1e-10), then a
  * polish: the active rows and face found at several thresholds, x purified onto them and the
- * dual rebuilt from the KKT system, kept where it tightens the certificate.  Where the
- * minimiser is not unique the path's limit, the analytic centre of the optimal face, is
- * returned.  Problems: each sequence's prefixes n = 0..T (all_prefixes = 1, actions
+ * dual rebuilt from the KKT system.  The path's own x is kept whenever that dual certifies it
+ * (gap <= 1e-9·(1 + obj)); the purified x replaces it only where x alone does not certify and
+ * the purified point tightens the certificate.  So where the minimiser is not unique the
+ * path's limit, the analytic centre of the optimal face, is returned.  Problems: each sequence's prefixes n = 0..T (all_prefixes = 1, actions
  * [B][T+1][d] as compute_prefix_actions :280-303 returns; actions[b][0] = 0) or n = T only
  * (all_prefixes = 0, [B][1][d]: the comparator).  obj [B][NP] (nullable) = ½Σ|r| at x
  * (for n = T: the comparator loss, exact_ftl.py:224-227, in butterfly order); gap [B][NP]

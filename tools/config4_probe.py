@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--runs", type=int, default=32768)
     ap.add_argument("--sizes", default="2048,2731,2979,3072")
     ap.add_argument("--T", type=int, default=10000)
+    ap.add_argument("--modes", default="32:0:1,32:0:0,64:0:1,64:1:1",
+                    help="lanes:trailing:whole-wave-batches per g(T) call")
     a = ap.parse_args()
     import torch
     from online_convex_optimization_amd import engine
@@ -30,24 +32,28 @@ def main():
     free, total = torch.cuda.mem_get_info()
     print(json.dumps({"what": "hbm", "free_GiB": free / 2**30, "total_GiB": total / 2**30}), flush=True)
     engine.release_buffers()
-    ref = None
-    for bw in ("1", "0"):
+    import numpy as np
+    refs = {}
+    # (layout lanes, trailing, whole-wave batches): 32 x 32 sequential (the default), the same
+    # with equal batches, 64 x 16 sequential, 64 x 16 through the trailing pipeline
+    for lanes, trail, bw in [m.split(":") for m in a.modes.split(",")]:
+        os.environ["OCX_GT_1K_LANES"] = lanes
+        os.environ["OCX_TRAILING"] = trail
         os.environ["OCX_BATCH_WAVES"] = bw
         engine.gT_regrets(T, a.runs, d=d)  # warm: the same shape (grows the library's HBM buffers)
         t0 = time.perf_counter()
         reg = engine.gT_regrets(T, a.runs, d=d)
         dt = time.perf_counter() - t0
-        if ref is None:
-            ref = reg
-        import numpy as np
-        print(json.dumps({"what": "config4_gT", "T": T, "runs": a.runs, "d": d,
-                          "batch_waves": bw == "1", "seconds": dt,
+        ref = refs.setdefault(lanes, reg)
+        print(json.dumps({"what": "config4_gT", "T": T, "runs": a.runs, "d": d, "lanes": int(lanes),
+                          "trailing": trail == "1", "batch_waves": bw == "1", "seconds": dt,
                           "free_GiB_after": torch.cuda.mem_get_info()[0] / 2**30,
                           "timesteps_per_s": T * a.runs / dt,
-                          "same_regrets": bool(np.array_equal(reg, ref)),
+                          "same_regrets_as_first_of_layout": bool(np.array_equal(reg, ref)),
                           "g": engine.max_regret(reg)}), flush=True)
     engine.release_buffers()
-    os.environ.pop("OCX_BATCH_WAVES", None)
+    for k in ("OCX_BATCH_WAVES", "OCX_GT_1K_LANES", "OCX_TRAILING"):
+        os.environ.pop(k, None)
     for B in (int(x) for x in a.sizes.split(",") if x):
         try:
             X = engine.DeviceBatch(B, T, d)

@@ -36,6 +36,7 @@
 #   layout       tools/e2e_layout.py (generation + FTRL by lane layout, d = 64)
 #   smalld       tools/gt_small_d.py (g(T) layouts for 4 <= d < 64)
 #   smart        tools/smart_probe.py (SMART kernels)
+#   twin         tools/twin32_probe.py (the float32 twin's timings)
 #   exact        tools/exact_probe.py (the general exact comparator)
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -133,7 +134,7 @@ for step in "$@"; do
     python tools/pmc_summary.py "${O}_gwpmc1" "${O}_gwpmc2" "${O}_gwpmc3" --kernel ocx_gen_wave --by-grid > "${O}_genwaves_pmc.txt"
     cat "${O}_genwaves_pmc.txt" ;;
   config4)
-    timeout -k 10 400 python -u tools/config4_probe.py > "${O}_config4.jsonl" 2> "${O}_config4.err" || fail config4 $?
+    timeout -k 10 500 python -u tools/config4_probe.py ${C4ARGS:-} > "${O}_config4.jsonl" 2> "${O}_config4.err" || fail config4 $?
     cat "${O}_config4.jsonl" ;;
   gpusub)
     # a subset of the GPU suite: GPUSUB="-k expr" (or test files) chosen per call
@@ -156,6 +157,9 @@ for step in "$@"; do
   smart)
     timeout -k 10 400 python -u tools/smart_probe.py > "${O}_smart.jsonl" 2> "${O}_smart.err" || fail smart $?
     cut -c1-200 "${O}_smart.jsonl" ;;
+  twin)
+    timeout -k 10 400 python -u tools/twin32_probe.py > "${O}_twin.jsonl" 2> "${O}_twin.err" || fail twin $?
+    cut -c1-200 "${O}_twin.jsonl" ;;
   exact)
     timeout -k 10 400 python -u tools/exact_probe.py > "${O}_exact.jsonl" 2> "${O}_exact.err" || fail exact $?
     cut -c1-200 "${O}_exact.jsonl" ;;

@@ -4,12 +4,15 @@
 """
 import json
 import math
+import os
+import sys
 import time
 
 import numpy as np
 
-from online_convex_optimization_amd import algorithms as A
-from online_convex_optimization_amd import engine
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from online_convex_optimization_amd import algorithms as A  # noqa: E402
+from online_convex_optimization_amd import engine  # noqa: E402
 
 
 def timed(fn, reps=3):
