@@ -30,8 +30,7 @@ int ocx_test_gT_regrets_unclean(uint64_t base_seed, int64_t T, int64_t run0, int
  * between them, closed-form comparator.  regret [B] (device): bit-identical to one launch
  * for every sequence the closed form certifies; NaN for the others, and *bad (device int,
  * zeroed by the caller) set to 1.  Synchronises `stream`.  Butterfly layouts the pipelined
- * kernel takes (P in {8, 16, 32}, C in {4, 8, 16, 32}), and 64 x 16 (d = 1024, one sequence
- * per wave), whose chunks run the lean plain kernel. */
+ * kernel takes (P in {8, 16, 32}, C in {4, 8, 16, 32}). */
 int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const double* y_tiled,
                               double eta0, int64_t chunk_steps, double* regret, int* bad,
                               void* stream);

@@ -383,6 +383,9 @@ hipError_t launch_pipe_c(int P, const PipeArgs& a, int ftl, hipStream_t st) {
         case 8: return launch_pipe_cp<C, 8>(a, ftl, st);
         case 16: return launch_pipe_cp<C, 16>(a, ftl, st);
         case 32: return launch_pipe_cp<C, 32>(a, ftl, st);
+        case 64:  // one sequence per wave: d = 1024 at 16 coordinates per lane only
+            if constexpr (C == 16) return launch_pipe_cp<16, 64>(a, ftl, st);
+            return hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }
@@ -427,11 +430,10 @@ PipeArgs pipe_args(const ocx_layout* L, const double* zt, const double* yt, doub
 // butterfly layouts keep the plain kernel.
 bool ocx_pipe_supported(const ocx_layout* L) {
     // T < 2^30: the step counter is a 32-bit int (ocx_ring_loop<..., int>)
-    // (64 x 16 — one sequence per wave at d = 1024 — runs the lean plain kernel since round 6,
-    // ocx_alg_lean1k_kernel: the arithmetic the d = 1024 trailing pipeline shares)
     return !L->chain && L->T < ((int64_t)1 << 30) &&
-           ((L->P == 8 || L->P == 16 || L->P == 32) &&
-            (L->C == 4 || L->C == 8 || L->C == 16 || L->C == 32));
+           (((L->P == 8 || L->P == 16 || L->P == 32) &&
+             (L->C == 4 || L->C == 8 || L->C == 16 || L->C == 32)) ||
+            (L->P == 64 && L->C == 16));
 }
 
 hipError_t ocx_launch_alg_pipe(const ocx_layout* L, const double* zt, const double* yt, int ftl,
@@ -508,12 +510,6 @@ hipError_t ocx_launch_alg_pipe_chunk(const ocx_layout* L, const double* zt, cons
                                      int64_t tn, double* state, int* bad,
                                      unsigned long long* gmax, hipStream_t st) {
     if (L->G == 0 || tn <= 0) return hipSuccess;
-    // the 64 x 16 layout: the lean plain kernel's chunks (ocx_alg_lean1k_kernel)
-    if (ocx_lean1k_layout(L))
-        return state && onepass ? ocx_launch_alg_lean1k(L, zt, yt, eta0, reg, nullptr, nullptr,
-                                                        nullptr, 1, t0, tn, state, bad,
-                                                        t0 + tn >= L->T ? gmax : nullptr, st)
-                                : hipErrorInvalidValue;
     // onepass only: a chunk after the first cannot stream the second comparator pass
     if (t0 < 0 || t0 % 64 != 0 || t0 + tn > L->T || !state || !onepass || !ocx_pipe_supported(L))
         return hipErrorInvalidValue;

@@ -896,12 +896,6 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
     // lanes) 10.6 -> 7.9 (the FTRL kernel alone 1.36 -> 1.60 ms at d = 16;
     // profiles/r03_config1_layouts.jsonl, r03_gt_small_d.jsonl).
     if (lanes_per_seq == OCX_LANES_BEST && d >= 4 && d < 64) lanes_per_seq = d >= 16 ? 8 : (d >= 8 ? 4 : 2);
-    // d = 1024: OCX_GT_1K_LANES=64 takes the 64 x 16 layout (one sequence per wave), whose lean
-    // FTRL kernel lets the trailing pipeline pair it with the generator (round 6, tuning)
-    if (lanes_per_seq == OCX_LANES_BEST && d == 1024) {
-        const char* e = std::getenv("OCX_GT_1K_LANES");
-        if (e && std::atoi(e) == 64) lanes_per_seq = 64;
-    }
     DevCtx* cx;
     if (int rc = ctx_enter(device, &cx)) return rc;
     std::lock_guard<std::mutex> lk(cx->mu);
@@ -1046,16 +1040,7 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
             c2 = (R + nb2 - 1) / nb2;
             // and no more streams than fit beside the FTRL waves in one generator round
             const int64_t cap = ocx_trailing_max_batch(&Lp);
-            if (ocx_lean1k_layout(&Lp)) {
-                // one stream per generator wave: whole waves per SIMD (see above), the last
-                // batch the remainder
-                int dev = 0, cus = 256;
-                OCX_HIP(hipGetDevice(&dev));
-                OCX_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                const int64_t simds = 4 * (int64_t)cus;
-                const int64_t cw = std::min(cap, std::min<int64_t>(budget / per_trail, R) / simds * simds);
-                if (cw >= simds) c2 = cw;
-            } else if (c2 > cap) {
+            if (c2 > cap) {
                 const int64_t nb3 = (R + cap - 1) / cap;
                 c2 = (R + nb3 - 1) / nb3;
             }
@@ -1256,8 +1241,7 @@ int ocx_test_alg_pipe_chunked(const ocx_layout* L, const double* z_tiled, const 
                               void* stream) {
     StreamDevice sd_(stream);
     if (int rc = check_layout(L)) return rc;
-    if (!ocx_pipe_supported(L) && !ocx_lean1k_layout(L))
-        return fail(OCX_E_UNSUPPORTED, "not a pipelined butterfly layout (or 64 x 16)");
+    if (!ocx_pipe_supported(L)) return fail(OCX_E_UNSUPPORTED, "not a pipelined butterfly layout");
     if (chunk_steps <= 0 || chunk_steps % 64) return fail(OCX_E_INVALID, "chunk_steps: a multiple of 64");
     if (L->B > 0 && (!regret || !bad || !z_tiled || !y_tiled)) return fail(OCX_E_INVALID, "NULL buffer");
     const hipStream_t st = (hipStream_t)stream;

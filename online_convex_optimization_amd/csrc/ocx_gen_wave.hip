@@ -340,8 +340,6 @@ __device__ __forceinline__ void ws_set(WaveStream& w, const ocx_pcg64& g, ocx_u1
     if constexpr (LS) {
         w.C64v = vcopy128(w.C64);
         w.s = mul_add_u128(w.Ak, w.base, w.Dk);
-    } else {
-        w.C64v = vcopy128(w.C64);  // the double rounds' second slot (dead code elsewhere)
     }
 }
 
@@ -689,89 +687,13 @@ __device__ __attribute__((always_inline)) int zig_round(WaveStream& w, int need,
     return n;
 }
 
-// Double rounds of the d = 1024 rows (OCX_GEN_1K_DOUBLE, round 6).  At three waves per SIMD —
-// all the HBM budget lets a d = 1024 batch run — a wave's round is latency-bound (§3.2 of
-// the table lookup, the ballot → scalar parse → next-state readlane chain), so each
-// lane draws two: draw k (slot 0) and draw 64 + k (slot 1, A^64 times slot 0's state plus C64),
-// and the wave parses all 128 in stream order with one pass of the bit trick below.  The common
-// case — no tail draw, no two rejected draws side by side — is zig_round's bit-trick parse over
-// a 128-bit mask: every rejected draw k takes draw k + 1 as its wedge uniform (slot 0's draw 63
-// takes slot 1's draw 0), a rejected draw 127 is redrawn next time.  Any other pattern (≈7 % of
-// double rounds) drops slot 1 and runs zig_round's general path for slot 0 alone.  The normals,
-// the draws consumed and so the stream are zig_round's, bit for bit.  Returns the normals
-// appended (ring: the d = 1024 ring, no wrap, slot map rix<SW>).
-#ifndef OCX_GEN_1K_DOUBLE
-#define OCX_GEN_1K_DOUBLE 0
-#endif
-template <int SW>
-__device__ __attribute__((always_inline)) int zig_round2(WaveStream& w, const ZigTables<false>& tb,
-                                                         double* ring, unsigned head, int lane) {
-    const ocx_u128 s0 = mul_add_u128(w.Ak, w.base, w.Dk);
-    const ocx_u128 s1 = mul_add_u128(s0, kA64, w.C64v);  // draw 64 + k
-    const uint64_t r0 = xsl_rr(s0), r1 = xsl_rr(s1);
-    const int idx0 = (int)(r0 & 0xff), idx1 = (int)(r1 & 0xff);
-    const uint64_t rabs0 = ((r0 >> 8) >> 1) & kMask52, rabs1 = ((r1 >> 8) >> 1) & kMask52;
-    uint64_t ki0, ki1;
-    double wi0, wi1;
-    zig_lookup(tb, idx0, ki0, wi0);
-    zig_lookup(tb, idx1, ki1, wi1);
-    double x0 = u52_to_double(rabs0) * wi0, x1 = u52_to_double(rabs1) * wi1;
-    x0 = __hiloint2double(__double2hiint(x0) ^ (int)(((uint32_t)r0 & 0x100u) << 23), __double2loint(x0));
-    x1 = __hiloint2double(__double2hiint(x1) ^ (int)(((uint32_t)r1 & 0x100u) << 23), __double2loint(x1));
-    const uint64_t rej0 = ballot(!(rabs0 < ki0)), rej1 = ballot(!(rabs1 < ki1));
-    if ((rej0 | rej1) == 0) {  // every draw accepted (≈14 %)
-        ring[rix<SW>(head + (unsigned)lane)] = x0;
-        ring[rix<SW>(head + 64u + (unsigned)lane)] = x1;
-        w.base = rl128(s1, 63);
-        return 128;
-    }
-    const uint64_t tails = (rej0 & ballot(idx0 == 0)) | (rej1 & ballot(idx1 == 0));
-    const uint64_t adj = (rej0 & (rej0 << 1)) | (rej1 & ((rej1 << 1) | (rej0 >> 63)));
-    if (tails | adj)  // rare patterns: slot 0 alone, by the general path
-        return zig_round<true, true, false, SW, true>(w, 64, tb, ring, 2047, head, lane);
-    // wedge tests on every lane of a slot with rejections (WU: outcomes read off ballots)
-    const uint64_t rd1 = shfl_down1(r1);
-    uint64_t wacc0 = 0, wacc1 = 0;
-    if (rej0) {
-        uint64_t rn = shfl_down1(r0);
-        const uint64_t r1l0 = rl64(r1, 0);
-        if (lane == 63) rn = r1l0;  // draw 63's uniform: draw 64
-        const int i1 = idx0 ? idx0 : 1;
-        const double lhs = (tb.fi[i1 - 1] - tb.fi[i1]) * u53(rn) + tb.fi[i1];
-        const double a = -0.5 * x0 * x0;
-        const double e = (double)__expf((float)a);  // |rel err| < 1e-6 for a in [-7, 0]
-        wacc0 = rej0 & ballot(lhs < e * (1.0 - 1e-5));
-        const uint64_t unsure = rej0 & ~wacc0 & ~ballot(lhs > e * (1.0 + 1e-5));
-        if (unsure) {
-            bool ex = false;
-            if ((unsure >> lane) & 1) ex = wedge_exact(lhs, a);
-            wacc0 |= ballot(ex);
-        }
-    }
-    if (rej1) {
-        const int i1 = idx1 ? idx1 : 1;
-        const double lhs = (tb.fi[i1 - 1] - tb.fi[i1]) * u53(rd1) + tb.fi[i1];
-        const double a = -0.5 * x1 * x1;
-        const double e = (double)__expf((float)a);
-        wacc1 = rej1 & ballot(lhs < e * (1.0 - 1e-5));
-        const uint64_t unsure = rej1 & ~wacc1 & ~ballot(lhs > e * (1.0 + 1e-5));
-        if (unsure) {
-            bool ex = false;
-            if ((unsure >> lane) & 1) ex = wedge_exact(lhs, a);
-            wacc1 |= ballot(ex);
-        }
-    }
-    // every rejected draw consumes the next as its uniform; a rejected draw 127 is redone
-    const uint64_t cons0 = rej0 << 1, cons1 = (rej1 << 1) | (rej0 >> 63);
-    const bool redo = (rej1 >> 63) != 0;
-    const uint64_t emit0 = (~rej0 | (rej0 & wacc0)) & ~cons0;
-    const uint64_t emit1 = (~rej1 | (rej1 & wacc1)) & ~cons1 & (redo ? ~(1ULL << 63) : ~0ULL);
-    const int n0 = __builtin_popcountll(emit0);
-    if ((emit0 >> lane) & 1) ring[rix<SW>(head + (unsigned)mbcnt(emit0))] = x0;
-    if ((emit1 >> lane) & 1) ring[rix<SW>(head + (unsigned)n0 + (unsigned)mbcnt(emit1))] = x1;
-    w.base = rl128(s1, redo ? 62 : 63);
-    return n0 + __builtin_popcountll(emit1);
-}
+// Double rounds of the d = 1024 rows (round 6, measured and removed; git history keeps the
+// form): each lane drew draws k and 64 + k (A^64 times the first state plus C64) and the wave
+// parsed all 128 with zig_round's bit trick over a 128-bit mask, falling back to a single
+// round for a tail draw or two adjacent rejections.  Bit-identical; 1 024 / 2 048 / 3 072 x
+// 5 000 streams (1 / 2 / 3 waves per SIMD, 168 VGPRs): 29.7 / 36.5 / 49.4 ms against 32.8 /
+// 37.7 / 49.3 ms — the latency it hides is gone by three waves per SIMD, which is where every
+// d = 1024 batch runs (profiles/r06_gen1k_double_ab.jsonl).
 
 // The wedge tests of the pending list (see DF above), all at once: lane i tests entry i, in
 // NumPy's double arithmetic (the 1e-5 float-estimate margin, the exact comparison where too
@@ -987,8 +909,7 @@ __host__ __device__ constexpr int gen_block(int DF, bool LR, int OV = 0) {
 // wave) and tables (6 KB per block) admit six waves per SIMD in LDS; the default form keeps
 // the four-wave register budget (no spills), the few-stream form (LR) asks for six.
 #ifndef OCX_GENW_MIN_WAVES
-// (d = 1024 with double rounds: three, the most its batches run — 168 VGPRs)
-#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : ((DF) == 1024 ? (OCX_GEN_1K_DOUBLE ? 3 : 4) : (((DF) == 16 || (DF) == 32) ? 4 : 1)))
+#define OCX_GENW_MIN_WAVES_FOR(DF, LR) ((DF) == 64 ? ((LR) ? 6 : 4) : (((DF) == 1024 || (DF) == 16 || (DF) == 32) ? 4 : 1))
 #else
 #define OCX_GENW_MIN_WAVES_FOR(DF, LR) OCX_GENW_MIN_WAVES
 #endif
@@ -1290,13 +1211,9 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
             const int64_t pstep = st1k.kstep * kst;
             while (produced < total) {
 #if OCX_GEN_INNER
-                if (total - produced >= 1024u + (OCX_GEN_1K_DOUBLE ? 128u : 64u)) {  // a whole row still to draw
+                if (total - produced >= 1024u + 64u) {  // a whole row still to draw
                     do {
-#if OCX_GEN_1K_DOUBLE
-                        const int n = zig_round2<kSW>(w, tb, ring, head, lane);
-#else
                         const int n = zig_round<true, true, kF1k, kSW, true>(w, 64, tb, ring, kFlat, head, lane);
-#endif
                         produced += (uint32_t)n;
                         head += (unsigned)n;
                     } while (head < 1024u);
@@ -1371,14 +1288,7 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
                     // the row's reads above complete before these writes)
                     const unsigned ov = head - 1024u;
                     const double sp = ring[rix<kSW>(1024u + (lane < 63 ? lane : 63))];
-#if OCX_GEN_1K_DOUBLE
-                    // a double round spills up to 127 normals: the second half after the first
-                    const double sp2 = ring[rix<kSW>(1088u + (lane < 63 ? lane : 63))];
                     if ((unsigned)lane < ov) ring[rix<kSW>((unsigned)lane)] = sp;
-                    if ((unsigned)lane + 64u < ov) ring[rix<kSW>(64u + (unsigned)lane)] = sp2;
-#else
-                    if ((unsigned)lane < ov) ring[rix<kSW>((unsigned)lane)] = sp;
-#endif
                     head = ov;
                     ++t;
                 }
@@ -1520,8 +1430,7 @@ __global__ __launch_bounds__(gen_block(DF, LR, OV), OV ? OV : OCX_GENW_MIN_WAVES
 namespace {
 
 int ring_doubles(int64_t d, int DF, bool LR = false) {
-    // one row + the next row's first round (ocx_gen_wave_kernel); a double round spills 127
-    if (DF == 1024) return 1024 + (OCX_GEN_1K_DOUBLE ? 128 : 64);
+    if (DF == 1024) return 1024 + 64;  // one row + the next row's first round (ocx_gen_wave_kernel)
     // R rows + one round, the R row scales; the default form also the deferred-wedge list
     // (kPendMax 16-B entries) and one flag byte per ring slot
     if (DF == 64)

@@ -298,8 +298,7 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
 // chunks ran 9–13 ms beside the FTRL chunks against 7.3 ms alone (profiles/r05_trail_c4*.jsonl,
 // DESIGN.md §3.8).
 bool ocx_trailing_supported(const ocx_layout* L) {
-    return (ocx_pipe_lean_supported(L) || ocx_lean1k_layout(L)) && L->T >= 128 &&
-           L->T * L->d < ((int64_t)1 << 32);
+    return ocx_pipe_lean_supported(L) && L->T >= 128 && L->T * L->d < ((int64_t)1 << 32);
 }
 
 int64_t ocx_trailing_max_batch(const ocx_layout* L) {
@@ -308,8 +307,6 @@ int64_t ocx_trailing_max_batch(const ocx_layout* L) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         cus = 256;
     const int64_t simds = 4 * (int64_t)cus, S = L->S;
-    // d = 1024 (64 x 16): three 128-VGPR generator waves per SIMD beside one lean FTRL wave
-    if (ocx_lean1k_layout(L)) return 3 * simds;
     // generator waves that fit: 4 on a SIMD beside an FTRL wave, 6 on one without
     int64_t b = simds * 6;
     while (b > S) {

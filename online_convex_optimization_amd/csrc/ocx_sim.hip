@@ -227,165 +227,6 @@ __global__ __launch_bounds__(OCX_BLOCK, (MINW > 0 ? MINW : (C <= 16 ? OCX_ALG_MI
 }
 
 // ---------------------------------------------------------------------------
-// The lean d = 1024 FTRL kernel (round 6): the 64 x 16 layout (one sequence per wave, 16
-// coordinates per lane), FTRL, at most 128 VGPRs (a two-step ring), so that one wave fits on
-// a SIMD beside three 128-VGPR d = 1024 generator waves — the trailing pipeline's pairing at
-// d = 1024 (ocx_pipeline.hip).  Its step is ocx_alg_kernel's (the same device functions in the
-// same order), and it is the kernel ocx_launch_alg runs for that layout, so every path over the
-// layout shares its arithmetic.  A chunked run (state != nullptr: steps [t0, t0 + tn), t0 a
-// multiple of 64) carries θ, the loss and the `clean` flag through HBM between launches (word i
-// of lane l of sequence b at state[(b·18 + i)·64 + l]) and equals the whole run bit for bit; a
-// sequence the closed form cannot certify then gets a NaN regret and raises *bad (a chunked
-// run cannot stream the second comparator pass: the early rows may already hold the next
-// batch), while a whole run streams that pass as ocx_alg_kernel does.
-constexpr int kLean1kWords = 16 + 2;  // θ[16], cum, clean
-// Its register budget: 4 waves per SIMD (128 VGPRs, what three 128-VGPR generator waves leave
-// of a SIMD's 512).  It needs 160 without spills; at 128 it reloads parts of z_t from scratch,
-// which costs memory instructions, not the VALU the generator beside it is bound by.
-#ifndef OCX_LEAN1K_MINW
-#define OCX_LEAN1K_MINW 4
-#endif
-__global__ __launch_bounds__(64, OCX_LEAN1K_MINW) void ocx_alg_lean1k_kernel(
-    const double* __restrict__ zt, const double* __restrict__ yt, int64_t B, int64_t T, int64_t G,
-    double eta0, double* __restrict__ regret, double* __restrict__ cum_out,
-    double* __restrict__ comp_out, int* __restrict__ closed_out, int onepass, int64_t t0,
-    int64_t tn, double* __restrict__ state, int* __restrict__ bad,
-    unsigned long long* __restrict__ gmax) {
-    constexpr int C = 16, P = 64, K = C / 2, NB = 2;
-    const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)__builtin_amdgcn_readfirstlane((int)blockIdx.x);  // one sequence
-    if (g >= G) return;
-    const int64_t b = g;
-    const bool live = b < B;
-    const bool first = t0 == 0, last = t0 + tn >= T;
-    // uniform bases (g is readfirstlane'd): every load is an SGPR base plus the lane's offset
-    const ocx_d2* __restrict__ zg = reinterpret_cast<const ocx_d2*>(zt) + (g * T + t0) * 64;
-    const int64_t kst = G * T * 64;
-    const double* __restrict__ yp = yt + g * T + t0;
-    auto stw = [&](int i) -> double& { return state[(g * kLean1kWords + i) * 64 + lane]; };
-
-    double th[C];
-    double cum = 0.0;
-    bool clean = true;
-    if (first) {
-#pragma unroll
-        for (int j = 0; j < C; ++j) th[j] = 0.0;
-    } else {
-#pragma unroll
-        for (int j = 0; j < C; ++j) th[j] = stw(j);
-        cum = stw(C);
-        clean = stw(C + 1) != 0.0;
-    }
-    ocx_d2 zb[NB][K];
-    double yb[NB];
-    auto load = [&](int slot, int64_t tl) {
-        const ocx_d2* __restrict__ row = zg + tl * 64;  // uniform
-#pragma unroll
-        for (int k = 0; k < K; ++k) zb[slot][k] = row[k * kst + lane];
-        yb[slot] = yp[tl];
-    };
-    OcxScaleTable sct;  // re-keyed at t0 + 1 (a multiple of 64 plus one): the whole run's blocks
-    ocx_ring_loop<NB>(tn, load, [&](int u, int64_t tl) {
-        // ocx_ftrl_act_dot_sc's tree path with the action formed where it is used (x_j = sθ_j,
-        // then (sθ_j)·f if rescaled): the same products and sums, no x[] held across them
-        const double sc = ocx_ftrl_scale(sct, t0 + tl + 1, eta0, lane);
-        double a = 0.0, bq = 0.0, zz = 0.0;  // ||sθ||², z·sθ and (ocx_row_in_ball's) ||z||²
-#pragma unroll
-        for (int j = 0; j < C; ++j) {
-            const double zj = ocx_zj(zb[u], j);
-            const double xj = sc * th[j];
-            a += xj * xj;
-            bq += zj * xj;
-            zz = __builtin_fma(zj, zj, zz);
-        }
-        const double nsq = ocx_seq_sum<P>(a);
-        double q = ocx_seq_sum<P>(bq);
-        const bool inball = ocx_seq_sum<P>(zz) <= 1.0 + 1e-12;
-        if (nsq > 1.0) {
-            const double f = 1.0 / sqrt(nsq);
-            double aq = 0.0;
-#pragma unroll
-            for (int j = 0; j < C; ++j) aq += ocx_zj(zb[u], j) * ((sc * th[j]) * f);
-            q = ocx_seq_sum<P>(aq);
-        }
-        const double diff = q - yb[u];  // :106-111
-        cum += 0.5 * fabs(diff);
-        const double gq = ocx_grad(diff);
-        if (onepass) clean = clean & inball;
-        clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
-#pragma unroll
-        for (int j = 0; j < C; ++j) th[j] += gq * ocx_zj(zb[u], j);  // gq*z is exact
-    });
-    if (!last) {
-#pragma unroll
-        for (int j = 0; j < C; ++j) stw(j) = th[j];
-        stw(C) = cum;
-        stw(C + 1) = clean ? 1.0 : 0.0;
-        return;
-    }
-    // comparator (ocx_alg_kernel's: the closed form where certified, else the second pass)
-    const bool closed = onepass && (clean || !live);
-    double comp = 0.0;
-    if (__ballot(closed) != 0) {  // wave-uniform (one sequence)
-        double p[C];
-#pragma unroll
-        for (int j = 0; j < C; ++j) p[j] = th[j] * th[j];
-        const double nrm = sqrt(ocx_total<C, P, false>(p, lane));
-        comp = 0.5 * (double)T - nrm;
-    } else {
-        if (first) {
-            double xs[C];
-            ocx_action_ftl<C, P, false>(th, xs, lane);
-            const ocx_d2* __restrict__ z0 = reinterpret_cast<const ocx_d2*>(zt) + g * T * 64;
-            const double* __restrict__ y0 = yt + g * T;
-            auto load0 = [&](int slot, int64_t t) {
-                const ocx_d2* __restrict__ row = z0 + t * 64;
-#pragma unroll
-                for (int k = 0; k < K; ++k) zb[slot][k] = row[k * kst + lane];
-                yb[slot] = y0[t];
-            };
-            ocx_ring_loop<NB>(T, load0, [&](int u, int64_t) {
-                double p[C];
-#pragma unroll
-                for (int j = 0; j < C; ++j) p[j] = ocx_zj(zb[u], j) * xs[j];
-                const double qq = ocx_total_last<C, P, false>(p, lane);
-                comp += 0.5 * fabs(qq - yb[u]);
-            });
-            comp = ocx_comp_lane_value<P, false>(comp, lane);
-        } else {
-            comp = __builtin_nan("");
-            if (lane == 0 && bad) *bad = 1;
-        }
-    }
-    const double rg = cum - comp;
-    if (lane == 0 && live) {
-        if (gmax && rg > 0.0) atomicMax(gmax, (unsigned long long)__double_as_longlong(rg));
-        if (regret) regret[b] = rg;
-        if (cum_out) cum_out[b] = cum;
-        if (comp_out) comp_out[b] = comp;
-        if (closed_out) closed_out[b] = closed ? 1 : 0;
-    }
-}
-
-bool ocx_lean1k_layout(const ocx_layout* L) {
-    return !L->chain && L->P == 64 && L->C == 16 && L->T < ((int64_t)1 << 30);
-}
-
-hipError_t ocx_launch_alg_lean1k(const ocx_layout* L, const double* zt, const double* yt,
-                                 double eta0, double* reg, double* cum, double* comp,
-                                 int* closed_out, int onepass, int64_t t0, int64_t tn,
-                                 double* state, int* bad, unsigned long long* gmax,
-                                 hipStream_t st) {
-    if (L->G == 0 || tn <= 0) return hipSuccess;
-    if (!ocx_lean1k_layout(L) || t0 < 0 || t0 % 64 || t0 + tn > L->T) return hipErrorInvalidValue;
-    if ((t0 > 0 || t0 + tn < L->T) && !state) return hipErrorInvalidValue;  // chunks carry state
-    hipLaunchKernelGGL(ocx_alg_lean1k_kernel, dim3((unsigned)L->G), dim3(64), 0, st, zt, yt, L->B,
-                       L->T, L->G, eta0, reg, cum, comp, closed_out, onepass, t0, tn, state, bad,
-                       gmax);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // fast_algorithms.py:118-164 `_simulate_SMART_like_core`
 // ---------------------------------------------------------------------------
 template <int C, int P, bool CHAIN>
@@ -712,10 +553,6 @@ hipError_t ocx_launch_alg(const ocx_layout* L, const double* zt, const double* y
     }();
     if ((algo == 0 || algo == 1) && !cmp && !xl && !cmp_out && !no_pipe && ocx_pipe_supported(L))
         return ocx_launch_alg_pipe(L, zt, yt, algo, eta0, reg, cum, comp, regime, onepass, st);
-    // the 64 x 16 layout's FTRL: the lean kernel (the trailing pipeline's arithmetic at d = 1024)
-    if (algo == 0 && !cmp && !xl && !cmp_out && ocx_lean1k_layout(L))
-        return ocx_launch_alg_lean1k(L, zt, yt, eta0, reg, cum, comp, regime, onepass, 0, L->T,
-                                     nullptr, nullptr, nullptr, st);
     OCX_DISPATCH(launch_alg_cp, L, zt, yt, algo, eta0, cmp, reg, cum, comp, xl, cmp_out, regime,
                  onepass, norm, st)
 }

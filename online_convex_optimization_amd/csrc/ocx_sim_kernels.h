@@ -117,14 +117,6 @@ int64_t ocx_gen_resident_waves(int64_t d, int dev);  // streams the generator ru
 hipError_t ocx_launch_alg_range(const ocx_layout* L, const double* zt, const double* yt,
                                 double eta0, double* reg, int onepass, int64_t g0, int64_t gn,
                                 unsigned long long* gmax, hipStream_t st);
-// The 64 x 16 layout (d = 1024, one sequence per wave) and its lean FTRL kernel: whole runs
-// (t0 = 0, tn = T, state nullable) or chunks of the trailing pipeline (state: G·18·64 doubles)
-bool ocx_lean1k_layout(const ocx_layout* L);
-hipError_t ocx_launch_alg_lean1k(const ocx_layout* L, const double* zt, const double* yt,
-                                 double eta0, double* reg, double* cum, double* comp,
-                                 int* closed_out, int onepass, int64_t t0, int64_t tn,
-                                 double* state, int* bad, unsigned long long* gmax,
-                                 hipStream_t st);
 hipError_t ocx_launch_gen_gT(const ocx_layout* L, uint64_t base_seed, int64_t run0, double* zt,
                              double* ytl, hipStream_t st);
 // the g(T) sampler's normals unclipped (the float32 twin clips them itself)

@@ -168,22 +168,17 @@ def _capacity_limited(monkeypatch, gb):
 
 
 @pytest.mark.parametrize("T,d,runs,gb,chunks", [(2000, 64, 1000, 0.35, "8"), (700, 64, 900, 0.06, "3"),
-                                                (300, 64, 500, 0.02, "2"), (200, 64, 9000, 0.5, "2"),
-                                                (640, 1024, 130, 0.25, "4"), (300, 1024, 2100, 2.6, "3")])
+                                                (300, 64, 500, 0.02, "2"), (200, 64, 9000, 0.5, "2")])
 def test_trailing_equals_sequential(eng, monkeypatch, T, d, runs, gb, chunks):
     """Regrets (host and device-resident) and g(T) of the trailing path equal the sequential
     loop's bit for bit, over several batches and a smaller last one, and sampled sequences are
-    within the closed-form bar of the oracle.  The first three d = 64 cases' batches (< 4 096
-    runs) take the 16 x 4 layout, the fourth's (4 500 runs) 8 x 8; the d = 1024 cases the 64 x 16
-    layout (OCX_GT_1K_LANES=64) and its lean FTRL kernel, the second with batches of whole
-    generator waves (1 024 runs, the last one the remainder).  Each call is checked to have gone
-    through the trailing pipeline (ocx_test_trailing_batches)."""
+    within the closed-form bar of the oracle.  The first three cases' batches (< 4 096 runs)
+    take the 16 x 4 layout, the last one's (4 500 runs) 8 x 8; each call is checked to have
+    gone through the trailing pipeline (ocx_test_trailing_batches)."""
     import torch
     from online_convex_optimization_amd import _lib
     _capacity_limited(monkeypatch, gb)
     monkeypatch.setenv("OCX_TRAIL_CHUNKS", chunks)
-    if d == 1024:
-        monkeypatch.setenv("OCX_GT_1K_LANES", "64")
     out = {}
     for trail in ("0", "1"):
         monkeypatch.setenv("OCX_TRAILING", trail)

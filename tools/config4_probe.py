@@ -23,8 +23,9 @@ def main():
     ap.add_argument("--runs", type=int, default=32768)
     ap.add_argument("--sizes", default="2048,2731,2979,3072")
     ap.add_argument("--T", type=int, default=10000)
-    ap.add_argument("--modes", default="32:0:1,32:0:0,64:0:1,64:1:1",
-                    help="lanes:trailing:whole-wave-batches per g(T) call")
+    ap.add_argument("--modes", default="32:0:1,32:0:0",
+                    help="lanes:trailing:whole-wave-batches per g(T) call (64 / trailing 1: the "
+                         "round-6 64 x 16 trailing experiment, whose code git history keeps)")
     a = ap.parse_args()
     import torch
     from online_convex_optimization_amd import engine

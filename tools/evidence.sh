@@ -35,6 +35,7 @@
 #   sweep        tools/perf_extra.py sweep config4 (configs[3] g(T) sweep and configs[4])
 #   layout       tools/e2e_layout.py (generation + FTRL by lane layout, d = 64)
 #   smalld       tools/gt_small_d.py (g(T) layouts for 4 <= d < 64)
+#   smallpipe    tools/small_pipe_probe.py (configs[1]'s d = 16 / 32 g(T): sequential vs pipeline)
 #   smart        tools/smart_probe.py (SMART kernels)
 #   twin         tools/twin32_probe.py (the float32 twin's timings)
 #   exact        tools/exact_probe.py (the general exact comparator)
@@ -151,6 +152,9 @@ for step in "$@"; do
   layout)
     timeout -k 10 400 python -u tools/e2e_layout.py > "${O}_layout.jsonl" 2> "${O}_layout.err" || fail layout $?
     cut -c1-200 "${O}_layout.jsonl" ;;
+  smallpipe)
+    timeout -k 10 400 python -u tools/small_pipe_probe.py > "${O}_smallpipe.jsonl" 2> "${O}_smallpipe.err" || fail smallpipe $?
+    cut -c1-220 "${O}_smallpipe.jsonl" ;;
   smalld)
     timeout -k 10 400 python -u tools/gt_small_d.py > "${O}_smalld.jsonl" 2> "${O}_smalld.err" || fail smalld $?
     cut -c1-200 "${O}_smalld.jsonl" ;;
