@@ -218,7 +218,11 @@ hipError_t ocx_run_gen_sim_pipelined(const ocx_layout* L, uint64_t base_seed, in
     // sweep at T = 100 (1e6 runs) ran 3.70e9 -> 3.98e9 timesteps/s (g(T) alone 4.23e9 ->
     // 4.59e9) with four, T = 1e3 the same with one or four, and 16 was slower at T = 1e3
     // (profiles/r04_sweep_subrounds.jsonl).  OCX_PIPE_SUB_ROUNDS overrides (tuning).
-    int64_t rounds = std::max<int64_t>(1, std::min<int64_t>(4, 1000 / std::max<int64_t>(L->T, 1)));
+    // (round 6: by normals per stream, T·d, rather than T: d = 16 / 32 rows are short, and
+    // configs[1]'s 65 536 x 1e3 x 16 batch ran 5.60 / 5.13 / 5.01 ms with 1 / 2 / 4 rounds per
+    // sub-batch against 5.42 ms sequential; d = 32: 7.98 / 7.94 / 8.10 vs 9.66 ms,
+    // profiles/r06_small_pipe.jsonl.  d = 64 keeps 1000 / T.)
+    int64_t rounds = std::max<int64_t>(1, std::min<int64_t>(4, 64000 / std::max<int64_t>(L->T * L->d, 1)));
     if (const char* e = std::getenv("OCX_PIPE_SUB_ROUNDS")) rounds = std::max<int64_t>(1, std::atoll(e));
     int64_t sub = sub_seqs > 0 ? sub_seqs : (int64_t)cus * 4 * std::max(1, wps) * rounds;
     sub = std::max(unit, (sub + unit - 1) / unit * unit);
