@@ -422,9 +422,10 @@ int ocx_dev_max_regret(const double* regrets, int64_t B, double* gmax, void* str
  * max(0, max over every batch's regrets), bit-identical to the host loop.  Queued on
  * `stream`; complete when the stream reaches this point.
  *   Pipelined (the default where supported: d = 64 with the 8 x 8 or 16 x 4 butterfly
- * layout, and a batch of at least four generator rounds unless sub_seqs > 0 asks for it):
- * the batch is cut into sub-batches of sequences (sub_seqs, <= 0: one generator round, up
- * to four below T = 1000) and sub-batch i+1 is generated while the FTRL kernel reads
+ * layout, d = 16 / 32 with 8 lanes of 2 / 4 coordinates — the g(T) layouts — and a batch of
+ * at least four generator rounds unless sub_seqs > 0 asks for it): the batch is cut into
+ * sub-batches of sequences (sub_seqs, <= 0: generator rounds making about 64 000 normals per
+ * stream, one to four) and sub-batch i+1 is generated while the FTRL kernel reads
  * sub-batch i, the sub-batches alternating over two library streams per side (forked from
  * and joined to `stream` by events), the generator at four 96-VGPR waves per SIMD and the
  * FTRL kernel in a 128-VGPR form so both stay resident (csrc/ocx_pipeline.hip); consecutive
