@@ -199,7 +199,7 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * action (replay_exact_ftl :318-323; 0 for n = T), so Σ_n step_loss is exact FTL's cumulative
  * loss; info [B][NP] (int32, nullable) = the solve's status and Newton steps:
  *   info >= 0, bit OCX_EXACT_INFO_BREAKDOWN clear: converged (steps; 0: the empty prefix);
- *   info < 0: the 300-step cap ended the solve (-steps);
+ *   info < 0: the step cap (300 steps; 1000 for d > 64) ended the solve (-steps);
  *   bit OCX_EXACT_INFO_BREAKDOWN set: stopped where μ outran fp64 (a Newton decrement no
  *     centred step produces) at the last centre, after (info & 0xFFFFF) steps — accurate to
  *     that μ only.
@@ -209,7 +209,7 @@ int ocx_ftrl_vs_exact_batch_ex(const double* z, const double* y, int64_t B, int6
  * OCX_EXACT_BALL_MAX_D (else OCX_E_UNSUPPORTED).  Parity vs cvxpy: unpinned (validated
  * against scipy's HiGHS LPs and by the certificate). */
 #define OCX_EXACT_INFO_BREAKDOWN (1 << 20)
-#define OCX_EXACT_BALL_MAX_D 64
+#define OCX_EXACT_BALL_MAX_D 256
 int ocx_exact_ball_solve(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
                          int norm, int all_prefixes, double* actions, double* obj, double* gap,
                          double* step_loss, int32_t* info, int device);

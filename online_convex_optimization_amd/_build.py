@@ -24,9 +24,9 @@ ARCH = os.environ.get("OCX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["ocx_sim.hip", "ocx_alg_pipe.hip", "ocx_smart_wave.hip", "ocx_smart_closed.hip", "ocx_ftrl_exact.hip", "ocx_gen.hip",
            "ocx_gen_wave.hip", "ocx_stream.hip", "ocx_twin32.hip", "ocx_comp_blas.hip",
-           "ocx_exact_ball.hip", "ocx_exact_wide.hip", "ocx_pipeline.hip", "ocx_capi.hip"]
+           "ocx_exact_ball.hip", "ocx_exact_wide.hip", "ocx_exact_big.hip", "ocx_pipeline.hip", "ocx_capi.hip"]
 HEADERS = ["../../include/ocx_testing.h", "ocx_internal.h", "ocx_rng.h", "ocx_sim_kernels.h", "zig_tables.h",
-           "ocx_device_math.h", "ocx_dispatch.h"]
+           "ocx_device_math.h", "ocx_dispatch.h", "ocx_exact_src.h"]
 
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
           "-fno-fast-math", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]

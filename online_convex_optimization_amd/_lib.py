@@ -118,7 +118,7 @@ TEST_SIGNATURES = {
 }
 OCX_VERSION = 400  # include/ocx.h OCX_VERSION: the ABI these signatures describe
 OCX_ALG_CLIPPED_ROWS = 1
-OCX_EXACT_BALL_MAX_D = 64  # include/ocx.h
+OCX_EXACT_BALL_MAX_D = 256  # include/ocx.h
 OCX_ALG_CLOSED_COMPARATOR = 2
 OCX_ALG_TREE_SUMS = 4
 OCX_SMART_CLOSED_PREFIX = 8

@@ -428,6 +428,12 @@ hipError_t solve(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_prefi
         OCX_EB_CASE(6) OCX_EB_CASE(7) OCX_EB_CASE(8) OCX_EB_CASE(9) OCX_EB_CASE(10)
 #undef OCX_EB_CASE
         default:
+            // 64 < d <= 256: the system in HBM scratch, the solve and its polish
+            // (ocx_exact_big.hip)
+            if (d > 64)
+                return ocx_launch_exact_big(rs.z, rs.y, B, rs.T, d, rs.tiled, rs.P, rs.C, rs.S,
+                                            rs.G, norm, all_prefixes, actions, obj, gap,
+                                            step_loss, info, st);
             // 10 < d <= 64: the system in LDS, one coordinate per lane (ocx_exact_wide.hip)
             return ocx_launch_exact_wide(rs.z, rs.y, B, rs.T, d, rs.tiled, rs.P, rs.C, rs.S, rs.G,
                                          norm, all_prefixes, actions, obj, gap, step_loss, info,
@@ -440,7 +446,7 @@ hipError_t launch(const RowSrc& rs, int64_t B, int64_t d, int norm, int all_pref
                   double* actions, double* obj, double* gap, double* step_loss, int32_t* info,
                   hipStream_t st) {
     const hipError_t e = solve(rs, B, d, norm, all_prefixes, actions, obj, gap, step_loss, info, st);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || d > 64) return e;  // ocx_launch_exact_big polishes its own solves
     return ocx_launch_exact_polish(rs.z, rs.y, B, rs.T, d, rs.tiled, rs.P, rs.C, rs.S, rs.G, norm,
                                    all_prefixes, actions, obj, gap, step_loss, st);
 }

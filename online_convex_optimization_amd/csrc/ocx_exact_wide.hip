@@ -16,6 +16,7 @@
 // rows (from L2), bound by the VALU.
 #include <algorithm>
 
+#include "ocx_exact_src.h"
 #include "ocx_internal.h"
 #include "ocx_sim_kernels.h"
 
@@ -39,26 +40,6 @@ __device__ __forceinline__ double wsum(double v) { return ocx_seq_sum<64>(v); }
 // costs little; it orders the LDS traffic for the compiler as the memory model requires,
 // instead of relying on the wave's lockstep.
 __device__ __forceinline__ void lds_sync() { __syncthreads(); }
-
-// element (i, j) of sequence b's rows: row-major z [B][T][d] or the tiled layout
-struct WideSrc {
-    const double* z;
-    const double* y;
-    int64_t T, G;
-    int d, P, C, S, tiled;
-    __device__ __forceinline__ double zat(int64_t b, int64_t i, int j) const {
-        if (!tiled) return z[(b * T + i) * d + j];
-        const int64_t g = b / S;
-        const int s = (int)(b - g * S);
-        const int jl = j / C, jj = j - jl * C;
-        return z[((int64_t)(jj >> 1) * G + g) * T * 128 + i * 128 + 2 * (s * P + jl) + (jj & 1)];
-    }
-    __device__ __forceinline__ double yat(int64_t b, int64_t i) const {
-        if (!tiled) return y[b * T + i];
-        const int64_t g = b / S;
-        return y[(g * T + i) * S + (b - g * S)];
-    }
-};
 
 template <int DP, int NORM>
 __global__ __launch_bounds__(64) void ocx_exact_wide_kernel(
@@ -417,7 +398,11 @@ namespace {
 // interpolate (±½) but only as good as μ_end for the ones it does.  Where the optimum
 // interpolates rows (n > d real-valued rows: an LAD vertex; n < d rows fitted exactly) the
 // barrier certificate stayed near 1e-5 relative, and a zero-loss prefix kept ½Σ|r_i| ≈ 5e-8.
-// For each of seven threshold scales (the best is kept; every bound is valid):
+// For each of eleven threshold pairs (τ_x, τ_r) = (1e-8·s, 1e-7·s) for seven scales s, then
+// four with the coordinates' and the rows' scales apart — a near-degenerate bound (normal-cone
+// multiplier ν ≪ 1) leaves x about μ_end/ν = 1e-6 inside it while every interpolated row is
+// tight to 1e-9, so no joint scale finds both (round 6, d = 100 linf) — the best is kept and
+// every bound is valid:
 //   1. active set at x: rows with |r_i| <= τ_r (1 + |y_i|) (at most 64, 63 beside the cone
 //      row), and the ball's
 //      constraints that hold: l2 ||x|| = 1; linf |x_j| = 1 (those coordinates fixed at ±1);
@@ -475,6 +460,8 @@ __device__ void polish_cholesky_solve(double* K, double* sc, int lane, double rh
 // The bar under which the polish keeps the solver's own x: a decade inside the host's
 // acceptance bar (engine.EXACT_GAP_RTOL = 1e-8), so a kept x always passes it.
 constexpr double kKeepRtol = 1e-9;
+// threshold sweeps: seven joint scales, then four with the coordinates' and rows' apart
+constexpr int kSweeps = 11;
 
 template <int NORM>
 __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
@@ -526,10 +513,14 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
         return rr;
     };
 
-    for (int sweep = 0; sweep < 7; ++sweep) {
+    for (int sweep = 0; sweep < kSweeps; ++sweep) {
         const double tsc = sweep == 0 ? 1.0 : (sweep == 1 ? 1e3 : (sweep == 2 ? 1e2 : (sweep == 3 ? 10.0 :
                            (sweep == 4 ? 1e4 : (sweep == 5 ? 0.1 : 0.01)))));
-        const double kTight = 1e-8 * tsc, kZero = 1e-7 * tsc;
+        // sweeps 7..10 scale the coordinates' and the rows' thresholds apart (a near-degenerate
+            // bound sits ~μ/ν from x while every row is still tight at 1e-7)
+            const double tx = sweep < 7 ? tsc : (sweep == 7 ? 1e2 : (sweep == 8 ? 1e4 : 1.0));
+            const double tr = sweep < 7 ? tsc : (sweep == 9 ? 1e2 : (sweep == 10 ? 1e4 : 1.0));
+            const double kTight = 1e-8 * tx, kZero = 1e-7 * tx, kZeroR = 1e-7 * tr;
         // ---- 1. the ball's constraints at x
         bool cone = false, fixed = false;
         double tgt = 0.0, crow = 0.0;  // fixed coordinate's value; the cone row's entry
@@ -568,7 +559,7 @@ __global__ __launch_bounds__(64) void ocx_exact_polish_kernel(
             if (lane < rows) {
                 rr = resid(lane, yv);
                 P0 += 0.5 * fabs(rr);
-                a = fabs(rr) <= kZero * (1.0 + fabs(yv));
+                a = fabs(rr) <= kZeroR * (1.0 + fabs(yv));
             }
             const uint64_t am = __ballot(a);
             const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),

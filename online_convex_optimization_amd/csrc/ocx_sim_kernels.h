@@ -88,6 +88,12 @@ hipError_t ocx_launch_exact_polish(const double* z, const double* y, int64_t B, 
                                    int64_t d, int tiled, int P, int C, int S, int64_t G, int norm,
                                    int all_prefixes, double* actions, double* obj, double* gap,
                                    double* step_loss, hipStream_t st);
+// the general exact comparator for 64 < d <= 256 (ocx_exact_big.hip): the solve and its
+// certificate polish, the system in a per-block HBM scratch matrix
+hipError_t ocx_launch_exact_big(const double* z, const double* y, int64_t B, int64_t T, int64_t d,
+                                int tiled, int P, int C, int S, int64_t G, int norm,
+                                int all_prefixes, double* actions, double* obj, double* gap,
+                                double* step_loss, int32_t* info, hipStream_t st);
 hipError_t ocx_launch_smart(const ocx_layout* L, const double* zt, const double* yt,
                             const double* th, double eta0, double* reg, int64_t* sw,
                             hipStream_t st);

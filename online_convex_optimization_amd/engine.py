@@ -200,7 +200,7 @@ def ftl_exact_batch(z, y, *, norm: str = "l2", lanes_per_seq: int = LANES_BEST, 
 
     Returns (cum_loss [B], comp_loss [B], comparator actions[T] [B, d], in_regime [B]);
     with ``check_regime`` the sequences outside the regime are solved by the general solver
-    (exact_ball_solve, d <= 64) — their numbers are the SOCP / LP's; without it they keep the
+    (exact_ball_solve, d <= 256) — their numbers are the SOCP / LP's; without it they keep the
     closed form's (not the solution there: callers must reject them)."""
     code = _norm_code(norm)
     z = _f64(z)
@@ -640,7 +640,7 @@ class DeviceBatch:
 
     def exact_general(self, norm: str = "l2", all_prefixes: bool = True):
         """The general exact-FTL solver (exact_ball_solve) on the resident batch
-        (ocx_dev_exact_ball_solve_tiled, d <= 64): a dict of device tensors ``actions``
+        (ocx_dev_exact_ball_solve_tiled, d <= 256): a dict of device tensors ``actions``
         [B, NP, d], ``obj``, ``gap``, ``step_loss`` [B, NP] and ``info`` (int32), NP = T+1
         or 1 (async on self.stream)."""
         torch = self.torch

@@ -27,7 +27,7 @@ minimiser maximises x·S_t over the ball (engine.ftl_prefix_actions_batch / ftl_
   Which point of the face cvxpy itself returns is solver-dependent: parity unpinned.
 * Outside the regime (a row beyond the dual ball, a label other than ±1 — the linf ball on
   the reference's own rows) the GPU solves the SOCP / LP itself: a log-barrier path with a
-  certified duality gap (engine.exact_ball_solve; d <= 64, larger d raises
+  certified duality gap (engine.exact_ball_solve; d <= 256, larger d raises
   ``NotImplementedError``).  A caller can still pass ``comparator_action`` /
   ``prefix_actions`` or any solver object with the reference's methods
   (``reset_buffers`` / ``append_row`` / ``solve_prefix_from_full``).

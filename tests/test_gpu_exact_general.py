@@ -213,7 +213,7 @@ def test_exact_driver_linf(eng):
 
 
 def test_general_limits_are_loud(eng):
-    z, y = _data(1, 2, 10, 65, clip=False)
+    z, y = _data(1, 2, 10, 257, clip=False)
     with pytest.raises(NotImplementedError):
         eng.exact_ball_solve(z, y, norm="linf")
     with pytest.raises(NotImplementedError):
@@ -364,3 +364,94 @@ def test_interpolating_optimum_certifies(eng, norm, d):
                 _, f_ref = lp_solve(z[b, :n], y[b, :n], norm)
                 assert abs(res["obj"][b, n] - f_ref) <= 1e-8 * (1.0 + f_ref), (b, n)
             assert res["obj"][b, n] - res["gap"][b, n] <= f_ref + 1e-9 * (1.0 + f_ref)
+
+
+# ---- 64 < d <= 256: the system in HBM scratch (ocx_exact_big.hip) -------------------------
+@pytest.mark.parametrize("norm", ["linf", "l1"])
+@pytest.mark.parametrize("d,T,clip,labels,prefixes", [(100, 130, True, "pm1", True),
+                                                      (65, 80, False, "real", True),
+                                                      (256, 300, True, "pm1", False),
+                                                      (256, 60, False, "real", False)])
+def test_big_lp_matches_highs(eng, norm, d, T, clip, labels, prefixes):
+    """d in {65, 100, 256}: the linf / l1 balls against HiGHS with the certificate, all
+    prefixes where the batch is small (the reference's cvxpy has no dimension limit,
+    exact_ftl.py:119-128).  Parity with cvxpy: unpinned."""
+    B = 2
+    z, y = _data(5 * d + (norm == "l1"), B, T, d, clip=clip, labels=labels)
+    res = eng.exact_ball_solve(z, y, norm=norm, all_prefixes=prefixes)
+    NP = T + 1 if prefixes else 1
+    assert res["actions"].shape == (B, NP, d)
+    # every problem (every prefix) finished and certifies to 1e-8 (engine.check_certificates)
+    assert eng.check_certificates(res["obj"], res["gap"], res["info"]) <= 1e-8 * (1.0 + res["obj"].max())
+    ns = [n for n in (1, 2, d // 2, d, d + 1, T) if n <= T] if prefixes else [T]
+    for b in range(B):
+        if prefixes:
+            assert np.all(res["actions"][b, 0] == 0.0)
+        for n in ns:
+            k = n if prefixes else 0
+            x_lp, f_lp = lp_solve(z[b, :n], y[b, :n], norm)
+            x = res["actions"][b, k]
+            f = res["obj"][b, k]
+            assert _norm_of(x, norm) <= 1.0 + 1e-12
+            assert abs(objective(z[b, :n], y[b, :n], x) - f) <= 1e-11 * (1.0 + f)
+            assert abs(f - f_lp) <= 1e-7 * (1.0 + f_lp), (b, n, f, f_lp)
+            _check_certificate(res, f_lp, b, k, gap_rtol=1e-8)
+        if prefixes:
+            for n in (0, d // 2, T - 1):
+                q = 0.0
+                for j in range(d):
+                    q = q + z[b, n, j] * res["actions"][b, n, j]
+                assert res["step_loss"][b, n] == 0.5 * abs(q - y[b, n])
+
+
+@pytest.mark.parametrize("d", [100, 256])
+def test_big_l2_vs_slsqp(eng, d):
+    B, T = 2, 40
+    z, y = _data(190 + d, B, T, d, clip=True, labels="real")
+    z *= 2.5                                                      # rows outside the ball
+    res = eng.exact_ball_solve(z, y, norm="l2", all_prefixes=False)
+    for b in range(B):
+        x_s, f_s = socp_solve(z[b], y[b])
+        f = res["obj"][b, 0]
+        assert np.linalg.norm(res["actions"][b, 0]) <= 1.0 + 1e-12
+        assert f <= f_s + 1e-9 * (1.0 + f_s), b                   # no worse than SLSQP
+        _check_certificate(res, f_s, b, 0, gap_rtol=1e-8)
+
+
+@pytest.mark.parametrize("norm", ["linf", "l1", "l2"])
+def test_big_interpolating_optimum_certifies(eng, norm):
+    """n > d = 100 unclipped rows with real labels: the optimum interpolates up to 100 rows,
+    which the polish's active set (DP = 128 rows) holds; every prefix's certificate passes."""
+    d, T, B = 100, 140, 1
+    rng = np.random.default_rng(2000 + NORM_CODES[norm])
+    z = 3.0 * rng.standard_normal((B, T, d))
+    y = rng.standard_normal((B, T))
+    res = eng.exact_ball_solve(z, y, norm=norm, all_prefixes=True)
+    assert np.all(res["info"][:, 1:] > 0)
+    assert eng.check_certificates(res["obj"], res["gap"], res["info"]) <= 1e-8 * (1.0 + res["obj"].max())
+    for n in (d + 1, T):
+        if norm == "l2":
+            _, f_ref = socp_solve(z[0, :n], y[0, :n])
+            assert res["obj"][0, n] <= f_ref + 1e-9 * (1.0 + f_ref)
+        else:
+            _, f_ref = lp_solve(z[0, :n], y[0, :n], norm)
+            assert abs(res["obj"][0, n] - f_ref) <= 1e-8 * (1.0 + f_ref), n
+        assert res["obj"][0, n] - res["gap"][0, n] <= f_ref + 1e-9 * (1.0 + f_ref)
+
+
+def test_big_tiled_and_engine_paths(eng):
+    """d = 100: the tiled entry point equals the row-major one bit for bit, and the batched
+    FTRL-vs-exact path answers out of the regime with every solve certified."""
+    import torch
+    B, T, d = 3, 50, 100
+    z, y = _data(31, B, T, d, clip=True)
+    ref = eng.exact_ball_solve(z, y, norm="linf")
+    db = eng.DeviceBatch(B, T, d).pack(z, y)
+    g = db.exact_general("linf")
+    torch.cuda.synchronize()
+    for k in ("actions", "obj", "gap", "step_loss", "info"):
+        assert np.array_equal(g[k][:B].cpu().numpy(), ref[k]), k
+    host = eng.ftrl_vs_exact_batch(z, y, SQ2, norm="linf")
+    assert not host["in_regime"].any() and host["exact_gap_max"] < 1e-7
+    assert np.array_equal(host["cum_exact"], np.cumsum(ref["step_loss"][:, :T], axis=1)[:, -1])
+    assert np.array_equal(host["comp"], ref["obj"][:, T])
