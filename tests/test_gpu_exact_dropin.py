@@ -99,7 +99,7 @@ def test_exact_driver_loop_body(ef):
 def test_out_of_regime_general(ef):
     """Outside the closed form's regime the drop-in takes the general solver (round 2
     raised NotImplementedError; tests/test_gpu_exact_general.py checks the answers); d = 11
-    (beyond round 3's limit) now answers too, only d > 64 is unsupported."""
+    (beyond round 3's limit) and d = 65 (round 6) answer too, only d > 256 is unsupported."""
     z, y, _ = O.random_iid_sample(2025, 50, 0)
     a = ef.compute_prefix_actions(ef.ExactFTLNoClip(5, 50), 3.0 * z, y)
     assert a.shape == (51, 5) and np.all(np.linalg.norm(a, axis=1) <= 1.0 + 1e-12)
@@ -109,8 +109,11 @@ def test_out_of_regime_general(ef):
     a11 = ef.compute_prefix_actions(ef.ExactFTLNoClip(11, 20), zz, np.ones(20))
     assert a11.shape == (21, 11) and np.all(np.linalg.norm(a11, axis=1) <= 1.0 + 1e-12)
     zz = 3.0 * np.random.default_rng(0).standard_normal((20, 65))
+    a65 = ef.compute_prefix_actions(ef.ExactFTLNoClip(65, 20), zz, np.ones(20))
+    assert a65.shape == (21, 65) and np.all(np.linalg.norm(a65, axis=1) <= 1.0 + 1e-12)
+    zz = 3.0 * np.random.default_rng(0).standard_normal((20, 257))
     with pytest.raises(NotImplementedError):
-        ef.compute_prefix_actions(ef.ExactFTLNoClip(65, 20), zz, np.ones(20))
+        ef.compute_prefix_actions(ef.ExactFTLNoClip(257, 20), zz, np.ones(20))
 
 
 def test_prefix_actions_batch_lane_splits(ef):

@@ -266,8 +266,8 @@ def test_errors_are_loud(ocx):
     fa = ocx["fa"]
     with pytest.raises(ValueError):
         fa.simulate_alg(np.zeros((4, 2)), np.zeros(3), 0, 1.0)
-    with pytest.raises(NotImplementedError):   # labels 0: the general solver, d > 64
-        ocx["ef"].run_ftrl(np.zeros((4, 65)), np.zeros(4))
+    with pytest.raises(NotImplementedError):   # labels 0: the general solver, d > 256
+        ocx["ef"].run_ftrl(np.zeros((4, 257)), np.zeros(4))
 
 
 # ------------------------------------------------------------------ full-size properties
