@@ -71,11 +71,17 @@ __device__ __forceinline__ double qmax_abs(const double (&v)[Q]) {
 }
 
 // S (DP × DP SPD, lower triangle, column-major: (i, j) at S[j·LD + i]) ← its Cholesky factor
-// after Jacobi scaling (scales into sc[] and si); the same operations as ocx_exact_wide.hip's
-// LDS factorisation, element for element.  cl: LDS [DP], the factor's column k.
+// after Jacobi scaling (scales into sc[] and si).  Right-looking, eight columns per panel: the
+// panel's columns (rows i + 64 q in registers) are factorised among themselves, then the
+// trailing columns take the panel's eight updates in one read and one write, k in order —
+// every element sees the same fma(−L_ik, L_jk, ·) sequence, k = 0, 1, ..., as one column at a
+// time (ocx_exact_wide.hip's LDS factorisation), so the factor is that one's, bit for bit,
+// with an eighth of the passes over the trailing matrix.  cl: LDS [8][DP], the panel's factor
+// columns.
+constexpr int kPanel = 8;
 template <int Q>
 __device__ void big_factor(double* S, double* sc, double* cl, int lane, double (&si)[Q]) {
-    constexpr int DP = 64 * Q, LD = DP + 1;
+    constexpr int DP = 64 * Q, LD = DP + 1, NP = kPanel;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int i = lane + 64 * q;
@@ -94,55 +100,81 @@ __device__ void big_factor(double* S, double* sc, double* cl, int lane, double (
         }
     }
     lds_sync();
-    for (int k = 0; k < DP; ++k) {
-        double* ck = S + (int64_t)k * LD;
-        double s = ck[k];
-        s = s > kPivotFloor ? s : kPivotFloor;
-        const double l = sqrt(s), rd = 1.0 / l;
-        double lik[Q];
+    for (int k0 = 0; k0 < DP; k0 += NP) {
+        // the panel's columns k0 .. k0 + 7, rows i >= k0 (the others are never read)
+        double pc[NP][Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int i = lane + 64 * q;
-            lik[q] = i > k ? ck[i] * rd : 0.0;
-        }
-        lds_sync();  // every lane has read the pivot before lane k rewrites it
+        for (int u = 0; u < NP; ++u)
 #pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int i = lane + 64 * q;
-            if (i == k) ck[k] = l;
-            if (i > k) {
-                ck[i] = lik[q];
-                cl[i] = lik[q];
+            for (int q = 0; q < Q; ++q) {
+                const int i = lane + 64 * q;
+                pc[u][q] = i >= k0 + u ? S[(int64_t)(k0 + u) * LD + i] : 0.0;
+            }
+#pragma unroll
+        for (int u = 0; u < NP; ++u) {
+            const int k = k0 + u;
+            double s = ocx_readlane(qpick(pc[u], k >> 6), k & 63);
+            s = s > kPivotFloor ? s : kPivotFloor;
+            const double l = sqrt(s), rd = 1.0 / l;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int i = lane + 64 * q;
+                const double lik = i > k ? pc[u][q] * rd : 0.0;
+                pc[u][q] = i == k ? l : lik;  // the factor's column (0 above the diagonal)
+                cl[u * DP + i] = lik;
+            }
+            lds_sync();  // column k of the factor published
+            // the panel's later columns: fma(−L_ik, L_jk, S_ij), j = k0 + u2
+#pragma unroll
+            for (int u2 = u + 1; u2 < NP; ++u2) {
+                const double ljk = cl[u * DP + k0 + u2];
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const int i = lane + 64 * q;
+                    if (i >= k0 + u2) pc[u2][q] = __builtin_fma(-(i > k ? pc[u][q] : 0.0), ljk, pc[u2][q]);
+                }
             }
         }
-        lds_sync();  // column k of the factor published
-        // trailing update, four columns at a time (their loads issued together)
-        for (int j0 = k + 1; j0 < DP; j0 += 4) {
+#pragma unroll
+        for (int u = 0; u < NP; ++u)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int i = lane + 64 * q;
+                if (i >= k0 + u) S[(int64_t)(k0 + u) * LD + i] = pc[u][q];
+            }
+        // the trailing columns j >= k0 + 8 take the panel's eight updates, k in order; four
+        // columns' loads in flight
+        for (int j0 = k0 + NP; j0 < DP; j0 += 4) {
             double v[4][Q];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u;
+            for (int w = 0; w < 4; ++w) {
+                const int j = j0 + w;
                 const double* col = S + (int64_t)j * LD;
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int i = lane + 64 * q;
-                    v[u][q] = (j < DP && i >= j) ? col[i] : 0.0;
+                    v[w][q] = (j < DP && i >= j) ? col[i] : 0.0;
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int j = j0 + u;
+            for (int w = 0; w < 4; ++w) {
+                const int j = j0 + w;
                 if (j >= DP) break;
-                const double ljk = cl[j];
                 double* col = S + (int64_t)j * LD;
+#pragma unroll
+                for (int u = 0; u < NP; ++u) {
+                    const double ljk = cl[u * DP + j];
+#pragma unroll
+                    for (int q = 0; q < Q; ++q) v[w][q] = __builtin_fma(-pc[u][q], ljk, v[w][q]);
+                }
 #pragma unroll
                 for (int q = 0; q < Q; ++q) {
                     const int i = lane + 64 * q;
-                    if (i >= j) col[i] = __builtin_fma(-lik[q], ljk, v[u][q]);
+                    if (i >= j) col[i] = v[w][q];
                 }
             }
         }
-        lds_sync();
+        lds_sync();  // the trailing matrix and cl are done with before the next panel
     }
 }
 
@@ -183,10 +215,11 @@ __device__ void big_solve(const double* S, int lane, const double (&si)[Q], cons
     for (int q = 0; q < Q; ++q) out[q] = c[q] * si[q];
 }
 
-// LDS of both kernels: RC staged rows, then DP-vectors and the row weights
+// LDS of both kernels: RC staged rows, then DP-vectors, the row weights and the factor's
+// panel (barrier kernel: 3 vectors, polish: 5)
 template <int Q>
 constexpr size_t big_lds_bytes() {
-    return (size_t)(RC * (64 * Q + 1) + 7 * 64 * Q + 2 * 64) * sizeof(double) +
+    return (size_t)(RC * (64 * Q + 1) + (5 + kPanel) * 64 * Q + 2 * 64) * sizeof(double) +
            (size_t)64 * Q * sizeof(int);
 }
 
@@ -216,9 +249,9 @@ __global__ __launch_bounds__(64) void ocx_exact_big_kernel(
     double* xs = R + RC * LD;    // x (then the direction vector of a rank-1 term)
     double* vv = xs + DP;        // diagonal terms of the ball barrier
     double* sc = vv + DP;        // Jacobi scales
-    double* cl = sc + DP;        // the factor's column k
-    double* gw = cl + DP;        // row weights r/s
+    double* gw = sc + DP;        // row weights r/s
     double* hw = gw + 64;        // row weights μ/(s·rt)
+    double* cl = hw + 64;        // the factor's panel columns [8][DP]
     double* S = scratch + (int64_t)blockIdx.x * sstride;  // the system [DP][LD]
     double* W = S + (int64_t)DP * LD;                     // μ/(s·rt) of every row [T]
 
@@ -567,10 +600,10 @@ __global__ __launch_bounds__(64) void ocx_exact_big_polish_kernel(
     double* gs = xs + DP;        // g = Σ_{i∉A} λ_i z_i
     double* em = gs + DP;        // 1.0 where coordinate j's stationarity equation holds
     double* sc = em + DP;        // δ on fixed coordinates / the solve's scales / λ_A
-    double* cl = sc + DP;        // the factor's column k
-    double* ra = cl + DP;        // active rows' residuals at x, then their y
-    double* wv = ra + DP + DP;   // per-row weights of a staged chunk (after a spare DP)
-    int* act = reinterpret_cast<int*>(wv + 128);  // active row indices [DP]
+    double* ra = sc + DP;        // active rows' residuals at x, then their y
+    double* wv = ra + DP;        // per-row weights of a staged chunk
+    double* cl = wv + 128;       // the factor's panel columns [8][DP]
+    int* act = reinterpret_cast<int*>(cl + kPanel * DP);  // active row indices [DP]
     double* S = scratch + (int64_t)blockIdx.x * sstride;  // the Gram systems [DP][LD]
     double* A = S + (int64_t)DP * LD;                      // active rows (+ cone row) [DP][LD]
 

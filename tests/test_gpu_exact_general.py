@@ -455,3 +455,21 @@ def test_big_tiled_and_engine_paths(eng):
     assert not host["in_regime"].any() and host["exact_gap_max"] < 1e-7
     assert np.array_equal(host["cum_exact"], np.cumsum(ref["step_loss"][:, :T], axis=1)[:, -1])
     assert np.array_equal(host["comp"], ref["obj"][:, T])
+
+
+@pytest.mark.parametrize("d,B,T,norm", [(70, 5, 110, "linf"), (150, 3, 100, "l1")])
+def test_big_persistent_blocks_reuse_scratch(eng, d, B, T, norm):
+    """More problems than resident blocks (512 at DP = 128, 256 at DP = 256): each block solves
+    several problems in turn in the same scratch matrices, and every answer is the one the
+    problem gets alone (a one-sequence call), bit for bit, and certified."""
+    z, y = _data(77 + d, B, T, d, clip=False, labels="real")
+    res = eng.exact_ball_solve(z, y, norm=norm, all_prefixes=True)
+    assert B * (T + 1) > (512 if d <= 128 else 256)
+    eng.check_certificates(res["obj"], res["gap"], res["info"])
+    for b in (0, B - 1):
+        one = eng.exact_ball_solve(z[b:b + 1], y[b:b + 1], norm=norm, all_prefixes=True)
+        for k in ("actions", "obj", "gap", "step_loss", "info"):
+            assert np.array_equal(res[k][b], one[k][0]), (b, k)
+    for n in (d // 2, T):
+        _, f_lp = lp_solve(z[0, :n], y[0, :n], norm)
+        assert abs(res["obj"][0, n] - f_lp) <= 1e-8 * (1.0 + f_lp), n
