@@ -368,6 +368,12 @@ __device__ __forceinline__ void ws_sync_base(WaveStream& w) {
 #ifndef OCX_GEN_FAST_REJ
 #define OCX_GEN_FAST_REJ 1
 #endif
+// the single-rejection shortcut below in the d = 64 rows' flat rounds too, with lane states.
+// Re-measured in round 6 on the current form: bit-identical, 49.66 -> 50.83 ms at 32 768 x 1e4
+// x 64, 90.07 -> 90.50 ms at 4 900 x 1e5 (profiles/r06_gen_fastrej_flat_ab.jsonl).  Off.
+#ifndef OCX_GEN_FAST_REJ_FLAT
+#define OCX_GEN_FAST_REJ_FLAT 0
+#endif
 // d = 64 row loop: an inner loop of full rounds while a whole batch is still to draw
 #ifndef OCX_GEN_INNER
 #define OCX_GEN_INNER 1
@@ -495,7 +501,7 @@ __device__ __attribute__((always_inline)) int zig_round(WaveStream& w, int need,
         return 64;
     }
 #if OCX_GEN_FAST_REJ
-    if constexpr (FULL && !FLAT) {
+    if constexpr (FULL && (!FLAT || OCX_GEN_FAST_REJ_FLAT)) {
         // The common rejection round (≈3/4 of them): one rejected draw k < 63 that is not a
         // tail draw.  Its wedge test runs on every lane (no exec-mask branch; lanes other than
         // k compute values nobody reads), the outcome is read off two ballots, and the
@@ -521,7 +527,9 @@ __device__ __attribute__((always_inline)) int zig_round(WaveStream& w, int need,
                 const bool skip = lane == k + 1 || (!wa && lane == k);
                 if (RING && !skip)
                     ring[rix<SW>((head + (unsigned)lane - (lane > k + 1 ? sh : 0u)) & fmask)] = x;
-                w.base = rl128(s, 63);  // (not FLAT: no lane states)
+                // the round consumed all 64 draws (k < 63 takes draw k + 1 as its uniform)
+                if constexpr (LS) w.s = mul_add_u128(s, kA64, w.C64v);
+                else w.base = rl128(s, 63);
                 return wa ? 63 : 62;
             }
         }
