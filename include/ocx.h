@@ -17,7 +17,9 @@
  *     the HIP kernels and copy results back (synchronous).
  *   - "dev" entry points take device pointers in the engine's tiled HBM layout
  *     (see ocx_layout) and a hipStream_t passed as void* (NULL = default stream);
- *     they are asynchronous and capture-safe (no allocation, no sync).
+ *     they are asynchronous and capture-safe (no allocation, no sync) — except
+ *     ocx_dev_exact_ball_solve / _tiled at d > 64, which take their Newton systems' scratch
+ *     stream-ordered (hipMallocAsync / hipFreeAsync on the caller's stream; no sync).
  *   - All arithmetic is IEEE binary64 (dtype "f64").
  *   - lanes_per_seq selects how a sequence's d coordinates map onto lanes:
  *       0      auto: the fewest lanes that fill the GPU; partial sums combined by a
