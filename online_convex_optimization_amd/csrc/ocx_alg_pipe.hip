@@ -235,7 +235,7 @@ __device__ __forceinline__ void alg_pipe_body(const PipeArgs& a) {
             an = __builtin_fma(ocx_zj(zn, j), th[j], an);
             bn = __builtin_fma(ocx_zj(zn, j), zj, bn);
         }
-        if (a.onepass) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
+        if (ocx_check_rows(a.onepass)) clean = clean & (ocx_seq_sum<P>(w) <= 1.0 + 1e-12);  // row t in ball
         // (at t = T-1, zn is the clamped look-ahead: A and Bz are then never used)
         V = zth;
         W = w;

@@ -526,9 +526,10 @@ int ocx_dev_gen_simulate(const ocx_layout* L, uint64_t base_seed, int64_t run0, 
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(gmax);
     if (acc) OCX_HIP(launch_zero_u64(acc, st));  // +0.0
     if (nbatch == 0 || L->B == 0 || L->T == 0) return OCX_OK;
-    // the sampler's rows are clipped: the closed-form comparator unless the caller asks for
-    // the reference's streamed pass (the bit-exact modes)
-    const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 1;
+    // the sampler's rows are clipped (by construction: no per-row check, ocx_check_rows): the
+    // closed-form comparator unless the caller asks for the reference's streamed pass (the
+    // bit-exact modes)
+    const int onepass = (flags & OCX_GENSIM_TWO_PASS) ? 0 : 2;
     if (!(flags & OCX_GENSIM_SEQUENTIAL) && ocx_pipeline_supported(L) && ocx_stream_fork_ok(st) &&
         (sub_seqs > 0 || ocx_pipeline_worth(L, pipe_wps()))) {
         OCX_HIP(ocx_run_gen_sim_pipelined(L, base_seed, run0, nbatch, z_tiled, y_tiled, eta0,
@@ -885,9 +886,10 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
     if (gmax) *gmax = 0.0;
     if (R == 0) return OCX_OK;
     if (!regrets && !gmax) return fail(OCX_E_INVALID, "NULL regrets");
-    // the sampler's rows are clipped: outside the bit-exact modes the comparator loss
-    // takes the closed form (ocx_dev_simulate_alg_ex), one HBM pass instead of two
-    const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 1;
+    // the sampler's rows are clipped (by construction: no per-row check, ocx_check_rows):
+    // outside the bit-exact modes the comparator loss takes the closed form
+    // (ocx_dev_simulate_alg_ex), one HBM pass instead of two
+    const int onepass = (lanes_per_seq == 1 || lanes_per_seq < 0) ? 0 : 2;
     // These batches are generated on device, and for 8 <= d < 64 the exact layout's one or
     // two lanes per sequence leave each generator wave (one stream) writing 16- or 32-B
     // pieces of a row into C/2 planes of the tile.  OCX_LANES_BEST takes butterfly lanes of

@@ -296,6 +296,17 @@ __device__ __forceinline__ void ocx_total2_last(const double (&p)[C], const doub
     }
 }
 
+// The one-pass comparator's `onepass` argument: 0 the streamed second pass; 1 the closed form
+// where certified, every row checked to lie in the ball; 2 the same for rows clipped by
+// construction (the engine's own g(T) sampler: z_t = x_t / max(1, ||x_t||), NumPy's rows bit for
+// bit), whose per-row check is skipped (OCX_CLIPPED_SKIP=0 keeps it: tuning A/B).
+#ifndef OCX_CLIPPED_SKIP
+#define OCX_CLIPPED_SKIP 1
+#endif
+__host__ __device__ __forceinline__ bool ocx_check_rows(int onepass) {
+    return onepass == 1 || (onepass == 2 && !OCX_CLIPPED_SKIP);
+}
+
 __device__ __forceinline__ double ocx_grad(double diff) {  // fast_algorithms.py:27-34
     return diff > 0.0 ? 0.5 : (diff < 0.0 ? -0.5 : 0.0);
 }

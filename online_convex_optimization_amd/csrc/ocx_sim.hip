@@ -125,7 +125,7 @@ __global__ __launch_bounds__(OCX_BLOCK, (MINW > 0 ? MINW : (C <= 16 ? OCX_ALG_MI
                 double gq = ocx_grad(diff);
                 // the closed form needs ||z_t|| <= 1 too: certified here, row by row,
                 // whatever the caller asserts (whole wave active: the test sums across lanes)
-                if (onepass) clean = clean & ocx_row_in_ball<C, P>(zb[u]);
+                if (ocx_check_rows(onepass)) clean = clean & ocx_row_in_ball<C, P>(zb[u]);
                 clean = clean && fabs(yb[u]) == 1.0 && gq == -0.5 * yb[u];
                 if (exact) {  // theta = −S_t: accumulate −y_t z_t; check the regime
                     linear = linear && ocx_dual_ok<C, P, CHAIN>(zb[u], norm, lane) &&
