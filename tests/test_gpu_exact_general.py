@@ -473,3 +473,24 @@ def test_big_persistent_blocks_reuse_scratch(eng, d, B, T, norm):
     for n in (d // 2, T):
         _, f_lp = lp_solve(z[0, :n], y[0, :n], norm)
         assert abs(res["obj"][0, n] - f_lp) <= 1e-8 * (1.0 + f_lp), n
+
+
+@pytest.mark.parametrize("norm", ["linf", "l1", "l2"])
+def test_big_degenerate_inputs(eng, norm):
+    """d = 100 edge cases: the empty horizon (T = 0: the empty prefix only, x = 0), all-zero rows
+    with ±1 labels (every x is optimal at ½Σ|y|; the path's centre is x = 0) and zero labels
+    (optimum 0 at x = 0) — every answer certified, as the d ≤ 64 kernels'."""
+    d = 100
+    res = eng.exact_ball_solve(np.zeros((2, 0, d)), np.zeros((2, 0)), norm=norm)
+    assert res["actions"].shape == (2, 1, d) and np.all(res["actions"] == 0.0)
+    assert np.all(res["obj"] == 0.0) and np.all(res["info"] == 0)
+    T = 12
+    y = np.where(np.arange(T) % 3 == 0, -1.0, 1.0)[None].repeat(2, axis=0)
+    res = eng.exact_ball_solve(np.zeros((2, T, d)), y, norm=norm)
+    eng.check_certificates(res["obj"], res["gap"], res["info"])
+    assert np.allclose(res["obj"][:, T], T / 2, rtol=0, atol=1e-12)
+    assert np.abs(res["actions"]).max() <= 1e-9
+    z, _ = _data(61, 2, T, d, clip=False)
+    res = eng.exact_ball_solve(z, np.zeros((2, T)), norm=norm)
+    eng.check_certificates(res["obj"], res["gap"], res["info"])
+    assert res["obj"].max() <= 1e-8
