@@ -1,7 +1,7 @@
 """configs[1]'s g(T) batch (65 536 runs x T = 1 000) at d = 16 / 32 through engine.gT_regrets:
 the sequential generate-then-simulate loop (OCX_PIPELINE=0) against the sub-batch pipeline
 (round 6 for these d) at several sub-batch sizes (OCX_PIPE_SUB_ROUNDS generator rounds per
-sub-batch) and generator waves per SIMD (OCX_PIPE_WPS).  One JSON line per setting, with a
+sub-batch) and generator waves per SIMD (OCX_PIPE_WPS; `def`: the library's own choice).  One JSON line per setting, with a
 bit-for-bit check against the sequential loop.
 
     python tools/small_pipe_probe.py [--d 16,32] [--runs 65536] [--T 1000]
@@ -32,6 +32,8 @@ def main():
                 os.environ.pop(k, None)
             if st == "seq":
                 os.environ["OCX_PIPELINE"] = "0"
+            elif st == "def":  # the library's own choice
+                pass
             else:
                 r, w = st.split(":")
                 os.environ["OCX_PIPE_SUB_ROUNDS"] = r
