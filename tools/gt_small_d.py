@@ -1,6 +1,9 @@
 """g(T) regrets through the C entry point (generation + FTRL per resident batch) at small d:
 OCX_LANES_BEST (butterfly lanes of two coordinates for 8 <= d < 64) against the exact layout
-(lanes_per_seq=1).  One JSON line per (d, mode)."""
+(lanes_per_seq=1).  One JSON line per (d, mode).  Then generation and FTRL apart per (d, lanes)
+of --split (d:lanes, default the layouts gT_regrets takes).
+    python tools/gt_small_d.py [--no-gt] [--split 8:4,16:8,32:8]"""
+import argparse
 import json
 import os
 import sys
@@ -11,10 +14,14 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--no-gt", action="store_true")
+    ap.add_argument("--split", default="8:4,16:8,32:8")
+    a = ap.parse_args()
     import numpy as np
     from online_convex_optimization_amd import engine
     T, runs = 1000, 65536
-    for d in (5, 8, 16, 32):
+    for d in (() if a.no_gt else (5, 8, 16, 32)):
         ref = None
         for name, lanes in (("best", engine.LANES_BEST), ("exact", 1)):
             engine.gT_regrets(T, runs, base_seed=0, d=d, lanes_per_seq=lanes)  # warm: same shape
@@ -30,8 +37,7 @@ def main():
     # generation and the FTRL pass apart, on the resident batch in the layout gT_regrets takes
     # (OCX_LANES_BEST: lanes of two coordinates, up to 8)
     import torch
-    for d in (8, 16, 32):
-        lanes = 8 if d >= 16 else 4
+    for d, lanes in ((int(x.split(":")[0]), int(x.split(":")[1])) for x in a.split.split(",")):
         X = engine.DeviceBatch(runs, T, d, lanes_per_seq=lanes)
         tg = tf = 1e9
         for _ in range(3):
