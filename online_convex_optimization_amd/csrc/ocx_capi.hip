@@ -46,6 +46,10 @@ struct DevBuf {
         cap = 0;
         return e;
     }
+    // Growing frees and maps again, which for the budget-sized batches (~250 GB) costs seconds.
+    // Buffers of a GiB or more therefore get a little slack (1/8, at most 4 GiB, in 256-MiB
+    // granules) when it fits, so the batches of successive calls — whose sizes differ by a few
+    // streams' bytes as T changes — reuse the allocation (tools/full_configs.py).
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) {
@@ -54,8 +58,19 @@ struct DevBuf {
             p = nullptr;
             cap = 0;
         }
-        hipError_t e = hipMalloc(&p, n ? n : 16);
-        if (e == hipSuccess) cap = n;
+        size_t want = n ? n : 16;
+        if (n >= ((size_t)1 << 30)) {
+            constexpr size_t kGran = (size_t)256 << 20;
+            const size_t pad = std::min(n / 8, (size_t)4 << 30);
+            want = (n + pad + kGran - 1) / kGran * kGran;
+        }
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess && want != n) {  // no room for the slack: the exact size
+            (void)hipGetLastError();
+            want = n;
+            e = hipMalloc(&p, want);
+        }
+        if (e == hipSuccess) cap = want;
         return e;
     }
     template <class T>
@@ -1026,6 +1041,15 @@ int gT_run(uint64_t base_seed, int64_t T, int64_t run0, int64_t R, int64_t d, do
         const char* pe = std::getenv("OCX_PIPELINE");
         const bool pipe = (!pe || std::atoi(pe) != 0) && ocx_pipeline_supported(&Lp) &&
                           ocx_pipeline_worth(&Lp, pipe_wps());
+        // A call of several batches holds its z tile at the whole budget (less two label
+        // tiles), not at its own batch: the batches of successive calls (a sweep over T at 1e6
+        // runs: 171 / 247 / 257 GB) differ, and growing an allocation of that size frees it and
+        // maps it again — a 3.7 s hipMalloc after the free, against 0.48 s for the first one
+        // (tools/batch_probe.py, profiles/r06_alloc_regrow.jsonl).
+        if (R > chunk) {
+            const int64_t zb = (int64_t)Lp.z_elems * 8, yb = (int64_t)Lp.y_elems * 8;
+            OCX_HIP(cx->zt.ensure((size_t)std::max<int64_t>(zb, budget - 2 * yb)));
+        }
         int64_t done = 0;
         // The batches the sub-batch pipeline leaves — capacity-limited (too few generator
         // rounds to cut: d = 64 at T = 1e5) or d != 64 (configs[4]'s d = 1024) — take the
